@@ -1,0 +1,199 @@
+"""bench.py — BASELINE.json's headline metric on MI355X: Mrays/s (+ wall-clock render time),
+cornellbox, path sampler, 1280x720 x 256 spp.
+
+A step = one full render of that workload (every pixel x every sample, bounces=8, clamp=10,
+seed 0x5EED) with the scene already resident in HBM: each rank traces its contiguous
+sample range [r*S/N, (r+1)*S/N) of all pixels (no data-path collective), then for N > 1 one
+RCCL reduce (sum of sample-weighted running means) gathers the image on rank 0 — the only
+exchange the path has. value = closest-hit scene queries of all ranks / time.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "julia-raytracer_amd"))
+
+METRIC = "Mrays/s + wall-clock render time, cornellbox 1280×720×256spp"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(c: dict, shade_bytes: int, quad_scene: bool) -> int:
+    """Algorithmic bytes of the trace launches: 32 B per BVH node pop,
+    64 B per instance visit, 48 B per triangle test (64 B per quad test), shade_bytes per
+    surface hit."""
+    return (32 * c["nodes"] + 64 * c["instances"] + (64 if quad_scene else 48) * c["prims"]
+            + shade_bytes * c["shades"])
+
+
+def shade_record_bytes(scene) -> int:
+    """Bytes fetched per shaded hit: instance shade record 64 + shape 32 + element ids 16 +
+    material 80 + positions 16/vertex (+ normals 16/vertex, texcoords 8/vertex, 4 texels per
+    texture lookup) — maximum over the scene's shapes (cornellbox: 240)."""
+    best = 0
+    for s in scene.shapes:
+        nv = 4 if len(s.quads) else 3
+        b = 64 + 32 + 16 + 80 + 16 * nv
+        if len(s.normals):
+            b += 16 * nv
+        if len(s.texcoords):
+            b += 8 * nv
+        best = max(best, b)
+    return best
+
+
+def cpu_baseline(scene_abi, params, width, height, nthreads, spp=2):
+    """Oracle (C restatement, oracle/jt_oracle.c) on host cores: bounded sample of the same
+    workload — all pixels, samples [0, spp)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from jtrace import abi
+    from oracle import Oracle  # the checker, timed as the CPU baseline only
+    orc = Oracle(abi)
+    ob = orc.build_bvh(scene_abi)
+    ol = orc.make_lights(scene_abi)
+    t0 = time.perf_counter()
+    _, _, _, _, cnt = orc.trace(scene_abi, ob, ol, params, width, height, 0, spp, nthreads=nthreads)
+    dt = time.perf_counter() - t0
+    return {"value": cnt["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": nthreads, "kind": "port",
+            "sample": f"{width}x{height} x {spp} spp (samples 0..{spp - 1}) of the bench workload, "
+                      f"{cnt['rays']} rays in {dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--sampler", default="path")
+    ap.add_argument("--scene", default=str(ROOT / "assets" / "scenes" / "cornellbox" / "cornellbox.json"))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-spp", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from jtrace import abi, sceneio, trace
+    from jtrace.cli import Params
+    lib = abi.load_library()
+    scene = sceneio.load_scene(args.scene)
+    sa = abi.SceneABI(scene)
+    params = Params(scene=args.scene, samples=args.spp, sampler=2 if args.sampler == "naive" else 1,
+                    width=args.width, height=args.height, device=local_rank, batch=args.spp)
+    jp = abi.make_params(params, 0)
+    bvh = trace.make_scene_bvh(sa, False, lib)
+    lights = trace.make_trace_lights(sa, lib)
+    state = trace.make_trace_state(sa, bvh, lights, jp, lib)
+    W, H, S = state.width, state.height, args.spp
+    s0, s1 = rank * S // world, (rank + 1) * S // world
+
+    img_t = None
+    if world > 1:
+        buf = state.device_buffers()
+
+        class _CAI:  # view the library's running-mean buffer as a torch tensor (no copy)
+            __cuda_array_interface__ = {"shape": (H * W * 4,), "typestr": "<f4",
+                                        "data": (buf.image, False), "version": 3}
+        img_t = torch.as_tensor(_CAI(), device=f"cuda:{local_rank}")
+
+    def step():
+        state.reset()
+        state.trace_range(s0, s1)
+        if world > 1:
+            part = img_t * float(s1 - s0)  # sample-weighted running mean of this shard
+            dist.reduce(part, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                part /= float(S)
+        return state.counters()
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rays = 0
+    kernel_ms = 0.0
+    agg = {k: 0 for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades", "launches")}
+    for _ in range(args.steps):
+        c = step()
+        for k in agg:
+            agg[k] += c[k]
+        kernel_ms += c["kernel_ms"]
+        rays += c["rays"]
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=f"cuda:{local_rank}")
+    if dist is not None:
+        tmax = t.clone()
+        dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+        elapsed, total_rays = float(tmax[0]), float(t[1])
+    else:
+        total_rays = float(rays)
+
+    if rank == 0:
+        value = total_rays / elapsed / 1e6
+        ms_per_step = elapsed / args.steps * 1e3
+        launches = max(1, agg["launches"])
+        avg_launch_s = kernel_ms / launches / 1e3
+        per_launch = {k: v / launches for k, v in agg.items()}
+        bytes_per_launch = algorithmic_bytes(per_launch, shade_record_bytes(scene),
+                                             any(len(s.quads) for s in scene.shapes))
+        achieved = bytes_per_launch / avg_launch_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "trace_kernel<1,16>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "bytes_per_launch": int(bytes_per_launch),
+                "bytes_per_ray": round(bytes_per_launch / max(1.0, per_launch["rays"]), 1)}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(sa, jp, W, H, args.cpu_threads, args.cpu_spp)
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic-free: the reference's own cornellbox scene (assets/scenes), seeded RNG",
+            "config": {"workload": f"cornellbox path {W}x{H}x{S}spp", "scene": "cornellbox",
+                       "sampler": args.sampler, "width": W, "height": H, "spp": S, "bounces": 8,
+                       "parallelism": f"sample-range shards x{world} + RCCL reduce"},
+            "render_s": round(ms_per_step / 1e3, 4),
+            "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 2),
+            "mlight_queries_per_s": round(agg["light_queries"] * world / elapsed / 1e6, 2),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    state.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

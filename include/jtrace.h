@@ -1,0 +1,280 @@
+/*
+ * jtrace.h — C-ABI drop-in boundary for the MI355X path-tracing hot path.
+ *
+ * The reference (Princic-1837592/julia-raytracer, pure Julia 1.8.3) has no FFI.
+ * Its natural seam is the per-batch call made by Jtrace.main:
+ *
+ *     trace_samples(state, scene, bvh, lights, params,
+ *                   bvh_stacks, bvh_sub_stacks, volume_stacks)   src/trace.jl:215-274
+ *
+ * This header exports exactly what a Julia `ccall` shim (julia-raytracer_amd/julia/
+ * JtraceHip.jl) or the Python `ctypes` harness binds to replace that call:
+ *
+ *   jt_create          ~ make_trace_state (src/trace.jl:189) + device upload of SceneData,
+ *                        SceneBvh and TraceLights (src/scene.jl:337, src/bvh.jl:59, src/trace.jl:111)
+ *   jt_trace_samples   == trace_samples for one batch (src/trace.jl:215)
+ *   jt_trace_range     == trace_samples over an explicit global sample range (multi-GPU shards)
+ *   jt_get_image       == get_image (src/trace.jl:676) — the running-mean RGBA buffer
+ *   jt_get_aovs        == TraceState.albedo / normal / hits (src/trace.jl:87-100)
+ *   jt_destroy / jt_last_error — lifetime and error reporting (the reference throws Julia exceptions)
+ *
+ * Host helpers (run on the CPU, no device needed) that restate the reference's host code
+ * for callers without their own:
+ *   jt_build_scene_bvh ~ make_scene_bvh (src/bvh.jl:66), split_middle / split_sah exact
+ *   jt_make_lights     ~ make_trace_lights (src/trace.jl:117)
+ *
+ * Conventions
+ *   - every function returns JT_OK (0) or a negative jt_status; nothing throws across the ABI;
+ *     jt_last_error() returns a thread-local message for the last failure on this thread.
+ *   - all indices are 0-based int32 (the reference uses 1-based Int64; the shim subtracts 1).
+ *     "none" ids (Julia invalid_id = -1, src/scene.jl:45) are -1 here too.
+ *   - frames are 12 floats, column-major x, y, z, o (Frame3f, src/math.jl:46-60).
+ *   - the caller owns every host array; jt_create deep-copies to the device, so host
+ *     arrays may be released after it returns (Julia: GC.@preserve around the ccall).
+ *   - a context is used by one host thread at a time; every call is synchronous.
+ */
+#ifndef JTRACE_H
+#define JTRACE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JT_ABI_VERSION 1
+
+typedef enum jt_status {
+    JT_OK = 0,
+    JT_ERR_INVALID = -1,      /* malformed input (bad id, size, NULL pointer) */
+    JT_ERR_UNSUPPORTED = -2,  /* input the reference cannot render either (see jt_create) */
+    JT_ERR_DEVICE = -3,       /* HIP runtime failure / no device */
+    JT_ERR_NOMEM = -4,        /* host or device allocation failed */
+    JT_ERR_STACK = -5,        /* BVH deeper than params.bvhstacksize (reference: BoundsError) */
+    JT_ERR_STATE = -6         /* call out of order (e.g. range outside [0, samples)) */
+} jt_status;
+
+/* MaterialType, in the order of the reference enum (src/scene.jl:191-200). */
+typedef enum jt_material_type {
+    JT_MATTE = 0,
+    JT_GLOSSY = 1,
+    JT_REFLECTIVE = 2,
+    JT_TRANSPARENT = 3,
+    JT_REFRACTIVE = 4,
+    JT_SUBSURFACE = 5,
+    JT_VOLUMETRIC = 6,
+    JT_GLTFPBR = 7
+} jt_material_type;
+
+/* Samplers, index into SAMPLER_TYPES = ["path", "naive"] (src/cli.jl:88). */
+typedef enum jt_sampler { JT_SAMPLER_PATH = 1, JT_SAMPLER_NAIVE = 2 } jt_sampler;
+
+/* CameraData (src/scene.jl:48-86), after the lookat conversion done by the loader. */
+typedef struct jt_camera {
+    float frame[12];
+    int32_t orthographic;
+    float lens, film, aspect, focus, aperture;
+} jt_camera;
+
+/* InstanceData (src/scene.jl:88-115). */
+typedef struct jt_instance {
+    float frame[12];
+    int32_t shape;     /* 0-based shape id */
+    int32_t material;  /* 0-based material id */
+} jt_instance;
+
+/* EnvironmentData (src/scene.jl:117-144). */
+typedef struct jt_environment {
+    float frame[12];
+    float emission[3];
+    int32_t emission_tex; /* -1 = none */
+} jt_environment;
+
+/* MaterialData (src/scene.jl:213-264). Texture ids are 0-based, -1 = none. */
+typedef struct jt_material {
+    int32_t type; /* jt_material_type */
+    float emission[3];
+    float color[3];
+    float roughness, metallic, ior;
+    float scattering[3];
+    float scanisotropy, trdepth, opacity;
+    int32_t emission_tex, color_tex, roughness_tex, scattering_tex, normal_tex;
+} jt_material;
+
+/* TextureData (src/scene.jl:146-162): RGBA, row-major, top row first.
+ * Exactly one of pixelsf (linear float, HDR) / pixelsb (8-bit) is non-NULL. */
+typedef struct jt_texture {
+    int32_t width, height;
+    int32_t linear;
+    const float* pixelsf;   /* width*height*4 floats or NULL */
+    const uint8_t* pixelsb; /* width*height*4 bytes or NULL */
+} jt_texture;
+
+/* ShapeData (src/shape.jl:13-48). Element arrays hold 0-based vertex ids.
+ * Per-vertex arrays may be NULL with count 0 (the reference's empty vectors). */
+typedef struct jt_shape {
+    int32_t npoints, nlines, ntriangles, nquads;
+    const int32_t* points;    /* npoints */
+    const int32_t* lines;     /* nlines*2 */
+    const int32_t* triangles; /* ntriangles*3 */
+    const int32_t* quads;     /* nquads*4 */
+    int32_t npositions;
+    const float* positions;   /* npositions*3 */
+    int32_t nnormals;
+    const float* normals;     /* nnormals*3 */
+    int32_t ntexcoords;
+    const float* texcoords;   /* ntexcoords*2 (v already flipped by the loader, src/shape.jl:88) */
+    int32_t ncolors;
+    const float* colors;      /* ncolors*4 */
+    int32_t nradius;
+    const float* radius;      /* nradius */
+} jt_shape;
+
+/* SceneData (src/scene.jl:337-356). */
+typedef struct jt_scene {
+    int32_t ncameras;
+    const jt_camera* cameras;
+    int32_t ninstances;
+    const jt_instance* instances;
+    int32_t nenvironments;
+    const jt_environment* environments;
+    int32_t nshapes;
+    const jt_shape* shapes;
+    int32_t ntextures;
+    const jt_texture* textures;
+    int32_t nmaterials;
+    const jt_material* materials;
+} jt_scene;
+
+/* BvhNode (src/bvh.jl:34-44), 0-based: `start` is the first child node (internal) or the
+ * first slot of `primitives` (leaf); axis is 0..2. 32 bytes, C-compatible. */
+typedef struct jt_bvh_node {
+    float bmin[3];
+    float bmax[3];
+    int32_t start;
+    int16_t num;
+    int8_t axis;
+    int8_t internal;
+} jt_bvh_node;
+
+/* BvhTree (src/bvh.jl:46-51). primitives[] are 0-based element (BLAS) or instance (TLAS) ids. */
+typedef struct jt_bvh_tree {
+    int32_t nnodes;
+    jt_bvh_node* nodes;
+    int32_t nprimitives;
+    int32_t* primitives;
+} jt_bvh_tree;
+
+/* SceneBvh (src/bvh.jl:59-64): the instance TLAS plus one BLAS per shape. */
+typedef struct jt_scene_bvh {
+    jt_bvh_tree tlas;
+    int32_t nshapes;
+    jt_bvh_tree* blas;
+} jt_scene_bvh;
+
+/* TraceLight (src/trace.jl:102-109): exactly one of instance / environment is >= 0. */
+typedef struct jt_light {
+    int32_t instance;
+    int32_t environment;
+    int32_t ncdf;
+    float* cdf;
+} jt_light;
+
+/* TraceLights (src/trace.jl:111-115). */
+typedef struct jt_lights {
+    int32_t nlights;
+    jt_light* lights;
+} jt_lights;
+
+/* Params (src/cli.jl:90-138) restricted to the fields the hot path reads, plus the
+ * build's extensions (seed, width/height override, device). */
+typedef struct jt_params {
+    int32_t camera;      /* 0-based camera id (find_camera result - 1) */
+    int32_t resolution;  /* --resolution; W,H derived from camera aspect as make_trace_state */
+    int32_t width;       /* extension: > 0 overrides W (with height) — aspect := W/H */
+    int32_t height;
+    int32_t samples;     /* --samples */
+    int32_t bounces;     /* --bounces */
+    int32_t sampler;     /* jt_sampler */
+    int32_t clamp;       /* --clamp, stored as Int by the reference (src/cli.jl:105) */
+    int32_t envhidden;
+    int32_t tentfilter;
+    int32_t nocaustics;
+    int32_t batch;       /* --batch */
+    int32_t bvhstacksize;
+    int32_t device;      /* HIP device ordinal for this context */
+    uint64_t seed;       /* extension: RNG seed; stream keyed by (seed, pixel, global sample) */
+} jt_params;
+
+/* Device counters accumulated over every launch of a context (diagnostic, exact). */
+typedef struct jt_counters {
+    uint64_t paths;          /* (pixel, sample) pairs traced */
+    uint64_t rays;           /* intersect_scene_bvh calls (closest-hit scene queries) */
+    uint64_t light_queries;  /* intersect_instance_bvh calls from sample_lights_pdf */
+    uint64_t nodes;          /* BVH node pops (TLAS + BLAS, both query kinds) */
+    uint64_t instances;      /* instance visits (TLAS leaf entries + light queries) */
+    uint64_t prims;          /* triangle / quad tests */
+    uint64_t shades;         /* surface hits shaded */
+    uint64_t launches;       /* kernel launches */
+    double kernel_ms;        /* summed device time of the trace launches (HIP events) */
+} jt_counters;
+
+/* Device pointers of a context's accumulators (for an in-place RCCL reduce). */
+typedef struct jt_device_buffers {
+    void* image;   /* float4[W*H]  running mean RGBA */
+    void* albedo;  /* float4[W*H]  running mean albedo (w unused) */
+    void* normal;  /* float4[W*H]  running mean normal (w unused) */
+    void* hits;    /* int64[W*H] */
+    int32_t width, height;
+    void* stream;  /* hipStream_t the context launches on */
+} jt_device_buffers;
+
+typedef struct jt_ctx jt_ctx;
+
+/* ---- library ---------------------------------------------------------------------- */
+const char* jt_version(void);
+int jt_abi_version(void);
+const char* jt_last_error(void);
+int jt_device_count(int32_t* out);
+
+/* ---- host helpers (CPU only) ------------------------------------------------------- */
+/* make_scene_bvh (src/bvh.jl:66-88): one BLAS per shape (make_shape_bvh :90) and the
+ * instance TLAS over transformed root boxes; split_middle (:185) or split_sah (:218). */
+int jt_build_scene_bvh(const jt_scene* scene, int32_t high_quality, jt_scene_bvh* out);
+void jt_free_scene_bvh(jt_scene_bvh* bvh);
+/* make_trace_lights (src/trace.jl:117-187). */
+int jt_make_lights(const jt_scene* scene, jt_lights* out);
+void jt_free_lights(jt_lights* lights);
+/* W,H as make_trace_state (src/trace.jl:189-197) or the width/height extension. */
+int jt_image_size(const jt_scene* scene, const jt_params* params, int32_t* width, int32_t* height);
+
+/* ---- device context ---------------------------------------------------------------- */
+/* Uploads scene, BVH and lights; allocates zeroed accumulators (make_trace_state).
+ * Rejects with JT_ERR_UNSUPPORTED what the reference cannot shade either: shapes with
+ * points (src/scene.jl:429), lines without normals (src/scene.jl:605), gltfpbr materials
+ * on instances (src/shading.jl:254-321 call undefined functions), and untextured
+ * environment lights (src/trace.jl:1003). */
+int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
+              const jt_params* params, jt_ctx** out);
+/* trace_samples (src/trace.jl:215-274): samples [n, min(n+batch, samples)), n += batch. */
+int jt_trace_samples(jt_ctx* ctx);
+/* Accumulate global samples [sample_begin, sample_end) into the running mean, in order.
+ * The running-mean weight of global sample s is 1/(s - first_sample + 1) where
+ * first_sample is the first sample this context ever traced (0 for a single device). */
+int jt_trace_range(jt_ctx* ctx, int32_t sample_begin, int32_t sample_end);
+int jt_get_samples(const jt_ctx* ctx, int32_t* samples);
+int jt_get_size(const jt_ctx* ctx, int32_t* width, int32_t* height);
+int jt_get_image(jt_ctx* ctx, float* rgba);                          /* W*H*4 */
+int jt_get_aovs(jt_ctx* ctx, float* albedo, float* normal, int64_t* hits); /* W*H*3, W*H*3, W*H */
+int jt_get_counters(jt_ctx* ctx, jt_counters* out);
+int jt_reset(jt_ctx* ctx);                                           /* zero accumulators, samples = 0 */
+int jt_get_device_buffers(jt_ctx* ctx, jt_device_buffers* out);
+int jt_synchronize(jt_ctx* ctx);
+void jt_destroy(jt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* JTRACE_H */

@@ -1,0 +1,382 @@
+// jt_device.h — device-side data layout and per-lane math of the MI355X path tracer.
+//
+// Everything here runs per lane inside the trace megakernel (jt_trace.hip). Each function
+// cites the reference (Princic-1837592/julia-raytracer) source it computes. Float contract
+// (DESIGN.md §Numerics): compiled with -ffp-contract=off (no FMA contraction, Julia's
+// evaluation order), Julia's NaN-propagating min/max, and — in the parity build
+// (JT_EXACT_MATH=1, the default) — transcendentals evaluated in double and rounded once,
+// which is how Julia's Float32 kernels compute them.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef JT_EXACT_MATH
+#define JT_EXACT_MATH 1
+#endif
+
+namespace jtd {
+
+// ------------------------------------------------------------------------------ layout in HBM
+// BVH node, 32 B = two 16-B loads: a = (bmin.xyz, start bits), b = (bmax.xyz, meta bits)
+// meta = num | axis << 16 | internal << 24. TLAS and all BLAS live in separate arrays;
+// BLAS `start` is a global node index (internal) or a global primitive-record slot (leaf).
+struct alignas(16) DNode {
+    float4 a, b;
+};
+// Traversal record of an instance, 64 B: inverse(frame, true) as 12 floats + ids.
+struct alignas(16) DInstTrav {
+    float4 i0, i1, i2;  // inv x.xyz y.x | y.yz z.xy | z.z o.xyz
+    int shape, blas_root, kind, prim_base;
+};
+// Shading record of an instance, 64 B: frame (12 floats) + material / shape ids.
+struct alignas(16) DInstShade {
+    float4 f0, f1, f2;
+    int material, shape, mat_type, pad;
+};
+enum { KIND_TRI = 0, KIND_QUAD = 1 };
+struct alignas(16) DShape {
+    int kind, blas_root, prim_base, idx_base;
+    int pos_base, nrm_base, tc_base, col_base;  // -1 = absent
+};
+struct alignas(16) DMaterial {
+    int type, emission_tex, color_tex, roughness_tex;
+    int scattering_tex, normal_tex, pad0, pad1;
+    float emission[3], roughness;
+    float color[3], metallic;
+    float scattering[3], ior;
+    float scanisotropy, trdepth, opacity, pad2;
+};
+struct alignas(16) DTexture {
+    int width, height, linear, is_float;
+    long long offset;  // texel index into texb (uchar4) or texf (float4)
+    long long pad;
+};
+struct alignas(16) DEnv {
+    float frame[12];
+    float inv[12];  // inverse(frame) rigid (src/scene.jl:906)
+    float emission[3];
+    int tex;
+};
+struct alignas(16) DLight {
+    int instance, environment, cdf_offset, ncdf;
+};
+
+struct DScene {
+    const DNode* tlas_nodes;
+    const int* tlas_prims;  // instance ids in leaf order
+    const DNode* blas_nodes;
+    const float4* prims;  // triangle: 3 float4 (p1|elem, p2, p3); quad: 4 float4 (p4.w = p3==p4)
+    const DInstTrav* inst_trav;
+    const DInstShade* inst_shade;
+    const DShape* shapes;
+    const float4* pos;
+    const float4* nrm;
+    const float2* tc;
+    const float4* col;
+    const int4* elems;  // triangle (a,b,c,0) / quad (a,b,c,d), global vertex ids
+    const DMaterial* materials;
+    const DTexture* textures;
+    const uchar4* texb;
+    const float4* texf;
+    const DEnv* envs;
+    const DLight* lights;
+    const float* cdf;
+    const float* srgb_lut;  // srgb_to_rgb(byte_to_float(b)), 256 entries (src/color.jl:12-23)
+    const float* byte_lut;  // byte_to_float(b)
+    int tlas_nnodes, nenvs, nlights, pad;
+};
+
+struct DCamera {
+    float frame[12];
+    int orthographic;
+    float lens, film, aspect, focus, aperture;
+};
+
+struct DParams {
+    DCamera cam;
+    int width, height;
+    int bounces, sampler;
+    float clamp;
+    int envhidden, tentfilter, nocaustics;
+    int first;  // running-mean origin: weight of sample s is 1/(s - first + 1)
+    int pad;
+    unsigned long long seed;
+};
+
+// ------------------------------------------------------------------------------ math (src/math.jl)
+static constexpr float pif = 3.14159265358979323846f;  // Float32(pi)
+static constexpr float ray_eps = 0.0001f;               // src/geometry.jl:34
+static constexpr float min_roughness = 0.03f * 0.03f;   // src/scene.jl:46
+
+struct v2 {
+    float x, y;
+};
+struct v3 {
+    float x, y, z;
+};
+struct v4 {
+    float x, y, z, w;
+};
+
+__device__ __forceinline__ v2 V2(float x, float y) { return v2{x, y}; }
+__device__ __forceinline__ v3 V3(float x, float y, float z) { return v3{x, y, z}; }
+__device__ __forceinline__ v4 V4(float x, float y, float z, float w) { return v4{x, y, z, w}; }
+__device__ __forceinline__ v3 operator+(v3 a, v3 b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 operator-(v3 a, v3 b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 operator*(v3 a, v3 b) { return V3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ v3 operator*(v3 a, float s) { return V3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ v3 operator/(v3 a, float s) { return V3(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ v3 operator-(v3 a) { return V3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ v4 operator+(v4 a, v4 b) { return V4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ v4 operator*(v4 a, float s) { return V4(a.x * s, a.y * s, a.z * s, a.w * s); }
+__device__ __forceinline__ bool is_zero(v3 a) { return a.x == 0 && a.y == 0 && a.z == 0; }
+__device__ __forceinline__ bool all_finite(v3 a) {
+    return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
+}
+__device__ __forceinline__ v3 xyz(float4 a) { return V3(a.x, a.y, a.z); }
+__device__ __forceinline__ v3 xyz(v4 a) { return V3(a.x, a.y, a.z); }
+
+// dot = sum(a .* b), left fold (src/math.jl:69)
+__device__ __forceinline__ float dot(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ v3 cross(v3 a, v3 b) {  // src/math.jl:112
+    return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ v3 normalize(v3 a) {  // src/math.jl:71-78
+    float l = __builtin_sqrtf(dot(a, a));
+    return l != 0 ? a / l : a;
+}
+__device__ __forceinline__ float length(v3 a) { return __builtin_sqrtf(dot(a, a)); }
+
+// Julia min/max for floats (base/math.jl): NaN-propagating, -0 < +0
+__device__ __forceinline__ float jl_min(float x, float y) {
+    bool c = (y < x) || (__builtin_signbit(y) && !__builtin_signbit(x));
+    return c ? (__builtin_isnan(x) ? x : y) : (__builtin_isnan(y) ? y : x);
+}
+__device__ __forceinline__ float jl_max(float x, float y) {
+    bool c = (y > x) || (!__builtin_signbit(y) && __builtin_signbit(x));
+    return c ? (__builtin_isnan(x) ? x : y) : (__builtin_isnan(y) ? y : x);
+}
+__device__ __forceinline__ float jl_clamp(float x, float lo, float hi) { return x > hi ? hi : (x < lo ? lo : x); }
+__device__ __forceinline__ int jl_clampi(int x, int lo, int hi) { return x > hi ? hi : (x < lo ? lo : x); }
+__device__ __forceinline__ float max3(v3 a) { return jl_max(jl_max(a.x, a.y), a.z); }
+
+#if JT_EXACT_MATH
+__device__ __forceinline__ float jl_sin(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float jl_cos(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ void jl_sincos(float x, float* s, float* c) {
+    double sd, cd;
+    sincos((double)x, &sd, &cd);
+    *s = (float)sd;
+    *c = (float)cd;
+}
+__device__ __forceinline__ float jl_atan(float x) { return (float)atan((double)x); }
+__device__ __forceinline__ float jl_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+__device__ __forceinline__ float jl_acos(float x) { return (float)acos((double)x); }
+__device__ __forceinline__ float jl_log(float x) { return (float)log((double)x); }
+__device__ __forceinline__ float jl_exp(float x) { return (float)exp((double)x); }
+#else
+__device__ __forceinline__ float jl_sin(float x) { return sinf(x); }
+__device__ __forceinline__ float jl_cos(float x) { return cosf(x); }
+__device__ __forceinline__ void jl_sincos(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ __forceinline__ float jl_atan(float x) { return atanf(x); }
+__device__ __forceinline__ float jl_atan2(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ float jl_acos(float x) { return acosf(x); }
+__device__ __forceinline__ float jl_log(float x) { return logf(x); }
+__device__ __forceinline__ float jl_exp(float x) { return expf(x); }
+#endif
+
+// Frame3f columns x, y, z, o packed in 12 floats
+struct fr3 {
+    v3 x, y, z, o;
+};
+__device__ __forceinline__ fr3 frame_from(const float* a) {
+    return fr3{V3(a[0], a[1], a[2]), V3(a[3], a[4], a[5]), V3(a[6], a[7], a[8]), V3(a[9], a[10], a[11])};
+}
+__device__ __forceinline__ fr3 frame_from(float4 a, float4 b, float4 c) {
+    return fr3{V3(a.x, a.y, a.z), V3(a.w, b.x, b.y), V3(b.z, b.w, c.x), V3(c.y, c.z, c.w)};
+}
+// transform_point / transform_vector / transform_direction / transform_normal (src/math.jl:80-129)
+__device__ __forceinline__ v3 transform_point(const fr3& f, v3 p) { return ((f.x * p.x + f.y * p.y) + f.z * p.z) + f.o; }
+__device__ __forceinline__ v3 transform_vector(const fr3& f, v3 b) { return (f.x * b.x + f.y * b.y) + f.z * b.z; }
+__device__ __forceinline__ v3 transform_direction(const fr3& f, v3 b) { return normalize(transform_vector(f, b)); }
+__device__ __forceinline__ v3 transform_normal(const fr3& f, v3 b) { return normalize(transform_vector(f, b)); }
+// Mat3f (3 columns) * Vec3f (src/math.jl:105)
+struct m3 {
+    v3 c1, c2, c3;
+};
+__device__ __forceinline__ v3 mul(const m3& m, v3 f) { return (m.c1 * f.x + m.c2 * f.y) + m.c3 * f.z; }
+// reflect / refract (src/math.jl:131-142)
+__device__ __forceinline__ v3 reflect(v3 w, v3 n) { return -w + n * (2 * dot(n, w)); }
+__device__ __forceinline__ v3 refract(v3 w, v3 n, float inv_eta) {
+    float cosine = dot(n, w);
+    float k = 1 + inv_eta * inv_eta * (cosine * cosine - 1);
+    if (k < 0) return V3(0, 0, 0);
+    return (-w) * inv_eta + n * (inv_eta * cosine - __builtin_sqrtf(k));
+}
+
+// ------------------------------------------------------------------------------ RNG (build)
+// PCG32 stream keyed by (seed, pixel, global sample); rand1f = 24-bit float in [0,1) like
+// Julia's rand(Float32). Stated in DESIGN.md §RNG and restated by oracle/jt_oracle.c.
+struct Rng {
+    unsigned long long state, inc;
+};
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ Rng rng_init(unsigned long long seed, int pixel, int sample) {
+    unsigned long long key = mix64(seed ^ mix64(((unsigned long long)(unsigned)pixel << 32) |
+                                                 (unsigned long long)(unsigned)sample));
+    Rng r;
+    r.inc = (mix64(key ^ 0xda3e39cb94b95bdbULL) << 1) | 1ULL;
+    r.state = (r.inc + key) * 6364136223846793005ULL + r.inc;
+    return r;
+}
+__device__ __forceinline__ unsigned rng_next(Rng& r) {
+    unsigned long long old = r.state;
+    r.state = old * 6364136223846793005ULL + r.inc;
+    unsigned xs = (unsigned)(((old >> 18) ^ old) >> 27);
+    unsigned rot = (unsigned)(old >> 59);
+    return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
+__device__ __forceinline__ float rand1f(Rng& r) { return (float)(rng_next(r) >> 8) * 0x1.0p-24f; }
+__device__ __forceinline__ v2 rand2f(Rng& r) {
+    float a = rand1f(r);
+    float b = rand1f(r);
+    return V2(a, b);
+}
+
+// ------------------------------------------------------------------------------ sampling.jl
+__device__ __forceinline__ v2 sample_disk(v2 ruv) {  // src/sampling.jl:12-16
+    float r = __builtin_sqrtf(ruv.y);
+    float phi = 2 * pif * ruv.x;
+    float s, c;
+    jl_sincos(phi, &s, &c);
+    return V2(c * r, s * r);
+}
+__device__ __forceinline__ float sample_hemisphere_cos_pdf(v3 normal, v3 direction) {  // :24-27
+    float cosw = dot(normal, direction);
+    return cosw <= 0 ? 0 : cosw / pif;
+}
+__device__ __forceinline__ int sample_uniform(int size, float r) {  // :29, 1-based
+    return jl_clampi((int)__builtin_truncf(r * (float)size) + 1, 1, size);
+}
+__device__ __forceinline__ float sample_uniform_pdf(int size) { return (float)(1.0 / (double)size); }  // :31
+__device__ __forceinline__ int upper_bound(const float* cdf, int n, float limit) {  // :42-56, 1-based
+    int idx = 0, l = 1, r = n;
+    while (l <= r) {
+        int m = (l + r) / 2;
+        if (cdf[m - 1] > limit) {
+            idx = m;
+            r = m - 1;
+        } else {
+            l = m + 1;
+        }
+    }
+    return idx;
+}
+__device__ __forceinline__ int sample_discrete(const float* cdf, int n, float r) {  // :33-37, 1-based
+    float last = cdf[n - 1];
+    r = jl_clamp(r * last, 0.0f, last - 0.00001f);
+    return jl_clampi(upper_bound(cdf, n, r), 1, n);
+}
+__device__ __forceinline__ float sample_discrete_pdf(const float* cdf, int idx1) {  // :39-40
+    return idx1 == 1 ? cdf[0] : cdf[idx1 - 1] - cdf[idx1 - 2];
+}
+__device__ __forceinline__ v2 sample_triangle(v2 ruv) {  // :58
+    return V2(1 - __builtin_sqrtf(ruv.x), ruv.y * __builtin_sqrtf(ruv.x));
+}
+
+// ------------------------------------------------------------------------------ geometry.jl
+// intersect_bbox (src/geometry.jl:96-105): Julia min/max; `t1 *= 1.00000024` is Float64.
+__device__ __forceinline__ bool intersect_bbox(v3 o, v3 dinv, float tmin, float tmax, const float4& a,
+                                               const float4& b) {
+    float mx = (a.x - o.x) * dinv.x, my = (a.y - o.y) * dinv.y, mz = (a.z - o.z) * dinv.z;
+    float Mx = (b.x - o.x) * dinv.x, My = (b.y - o.y) * dinv.y, Mz = (b.z - o.z) * dinv.z;
+    // equivalent to the Julia min/max chains: any NaN slab value culls (t0 or t1 is NaN), and
+    // signed zeros cannot change `t0 <= t1`; otherwise IEEE min/max agree with Julia's.
+    bool nan = __builtin_isnan(mx) | __builtin_isnan(my) | __builtin_isnan(mz) | __builtin_isnan(Mx) |
+               __builtin_isnan(My) | __builtin_isnan(Mz);
+    float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(mx, Mx), __builtin_fminf(my, My)),
+                                               __builtin_fminf(mz, Mz)),
+                               tmin);
+    float t1 = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fmaxf(mx, Mx), __builtin_fmaxf(my, My)),
+                                               __builtin_fmaxf(mz, Mz)),
+                               tmax);
+    return !nan && ((double)t0 <= (double)t1 * 1.00000024);
+}
+
+struct PrimHit {
+    float u, v, t;
+    bool hit;
+};
+// intersect_triangle (src/geometry.jl:206-236)
+__device__ __forceinline__ PrimHit intersect_triangle(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 p2, v3 p3) {
+    PrimHit miss{0, 0, __builtin_inff(), false};
+    v3 edge1 = p2 - p1, edge2 = p3 - p1;
+    v3 pvec = cross(d, edge2);
+    float det = dot(edge1, pvec);
+    if (det == 0) return miss;
+    float inv_det = 1.0f / det;
+    v3 tvec = o - p1;
+    float u = dot(tvec, pvec) * inv_det;
+    if (u < 0 || u > 1) return miss;
+    v3 qvec = cross(tvec, edge1);
+    float v = dot(d, qvec) * inv_det;
+    if (v < 0 || u + v > 1) return miss;
+    float t = dot(edge2, qvec) * inv_det;
+    if (t < tmin || t > tmax) return miss;
+    return PrimHit{u, v, t, true};
+}
+// intersect_quad (src/geometry.jl:238-258); `degenerate` = (p3 == p4), precomputed on the host
+__device__ __forceinline__ PrimHit intersect_quad(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 p2, v3 p3, v3 p4,
+                                                  bool degenerate) {
+    if (degenerate) return intersect_triangle(o, d, tmin, tmax, p1, p2, p4);
+    PrimHit i1 = intersect_triangle(o, d, tmin, tmax, p1, p2, p4);
+    PrimHit i2 = intersect_triangle(o, d, tmin, tmax, p3, p4, p2);
+    if (i2.hit) {
+        i2.u = 1 - i2.u;
+        i2.v = 1 - i2.v;
+    }
+    return i1.t < i2.t ? i1 : i2;
+}
+__device__ __forceinline__ v3 triangle_normal(v3 p1, v3 p2, v3 p3) { return normalize(cross(p2 - p1, p3 - p1)); }
+__device__ __forceinline__ v3 quad_normal(v3 p1, v3 p2, v3 p3, v3 p4) {
+    return normalize(triangle_normal(p1, p2, p4) + triangle_normal(p3, p4, p2));
+}
+// interpolate_triangle / interpolate_quad (src/geometry.jl:275-283)
+__device__ __forceinline__ v3 interp_tri(v3 p1, v3 p2, v3 p3, v2 uv) {
+    float w = (1 - uv.x) - uv.y;
+    return (p1 * w + p2 * uv.x) + p3 * uv.y;
+}
+__device__ __forceinline__ v2 interp_tri(v2 p1, v2 p2, v2 p3, v2 uv) {
+    float w = (1 - uv.x) - uv.y;
+    return V2((p1.x * w + p2.x * uv.x) + p3.x * uv.y, (p1.y * w + p2.y * uv.x) + p3.y * uv.y);
+}
+__device__ __forceinline__ v4 interp_tri(v4 p1, v4 p2, v4 p3, v2 uv) {
+    float w = (1 - uv.x) - uv.y;
+    return (p1 * w + p2 * uv.x) + p3 * uv.y;
+}
+template <class T>
+__device__ __forceinline__ T interp_quad(T p1, T p2, T p3, T p4, v2 uv) {
+    if (uv.x + uv.y <= 1) return interp_tri(p1, p2, p4, uv);
+    return interp_tri(p3, p4, p2, V2(1 - uv.x, 1 - uv.y));
+}
+// triangle_tangents_fromuv (src/geometry.jl:285-316)
+__device__ __forceinline__ void triangle_tangents_fromuv(v3 p1, v3 p2, v3 p3, v2 uv1, v2 uv2, v2 uv3, v3& tu, v3& tv) {
+    v3 p = p2 - p1, q = p3 - p1;
+    v2 s = V2(uv2.x - uv1.x, uv3.x - uv1.x);
+    v2 t = V2(uv2.y - uv1.y, uv3.y - uv1.y);
+    float div = s.x * t.y - s.y * t.x;
+    if (div != 0) {
+        tu = V3(t.y * p.x - t.x * q.x, t.y * p.y - t.x * q.y, t.y * p.z - t.x * q.z) / div;
+        tv = V3(s.x * q.x - s.y * p.x, s.x * q.y - s.y * p.y, s.x * q.z - s.y * p.z) / div;
+    } else {
+        tu = V3(1, 0, 0);
+        tv = V3(0, 1, 0);
+    }
+}
+
+}  // namespace jtd

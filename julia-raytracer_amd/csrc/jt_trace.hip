@@ -1,0 +1,1284 @@
+// jt_trace.hip — the MI355X (gfx950) path-tracing megakernel and the C-ABI device context.
+//
+// Replaces trace_samples (Princic-1837592/julia-raytracer src/trace.jl:215-274) and everything
+// it calls per (pixel, sample, bounce): trace_sample :584, trace_path :276 / trace_naive :471,
+// intersect_scene_bvh / intersect_shape_bvh / intersect_instance_bvh (src/bvh.jl:306-520),
+// scene evaluation (src/scene.jl:372-928), shading (src/shading.jl), sampling (src/sampling.jl).
+//
+// Design: one lane owns one pixel and loops over its samples with path
+// regeneration — a lane whose path terminated starts its next sample in the same loop
+// iteration in which other lanes continue bouncing, so the wave stays full. Two-level BVH
+// traversal is one loop over a unified per-lane stack in LDS (TLAS nodes, instance entries,
+// BLAS nodes) so that every lane does one stack pop per iteration whatever level it is at;
+// the traversal order (and hence hit tie-breaking) is exactly the reference's. The running
+// mean (lerp with w = 1/(s+1), src/trace.jl:631-648) is kept in registers across samples and
+// written once per launch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "jt_bsdf.h"
+#include "jt_device.h"
+#include "jt_internal.h"
+
+using namespace jtd;
+
+namespace {
+
+// ============================================================================ scene evaluation
+__device__ __forceinline__ fr3 inst_frame(const DScene& S, int inst) {
+    const DInstShade& r = S.inst_shade[inst];
+    return frame_from(r.f0, r.f1, r.f2);
+}
+
+// eval_position (src/scene.jl:435-476)
+__device__ __forceinline__ v3 eval_position(const DScene& S, int inst, int elem, v2 uv) {
+    const DInstShade& is = S.inst_shade[inst];
+    const DShape sh = S.shapes[is.shape];
+    const int4 e = S.elems[sh.idx_base + elem];
+    const fr3 f = frame_from(is.f0, is.f1, is.f2);
+    v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
+    if (sh.kind == KIND_TRI) return transform_point(f, interp_tri(p1, p2, p3, uv));
+    return transform_point(f, interp_quad(p1, p2, p3, xyz(S.pos[e.w]), uv));
+}
+// eval_element_normal (src/scene.jl:578-612)
+__device__ __forceinline__ v3 eval_element_normal(const DScene& S, int inst, int elem) {
+    const DInstShade& is = S.inst_shade[inst];
+    const DShape sh = S.shapes[is.shape];
+    const int4 e = S.elems[sh.idx_base + elem];
+    const fr3 f = frame_from(is.f0, is.f1, is.f2);
+    v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
+    if (sh.kind == KIND_TRI) return transform_normal(f, triangle_normal(p1, p2, p3));
+    return transform_normal(f, quad_normal(p1, p2, p3, xyz(S.pos[e.w])));
+}
+// eval_normal (src/scene.jl:525-576)
+__device__ __forceinline__ v3 eval_normal(const DScene& S, const DShape& sh, const int4& e, const fr3& f, v2 uv) {
+    if (sh.nrm_base < 0) {
+        v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
+        if (sh.kind == KIND_TRI) return transform_normal(f, triangle_normal(p1, p2, p3));
+        return transform_normal(f, quad_normal(p1, p2, p3, xyz(S.pos[e.w])));
+    }
+    const int b = sh.nrm_base - sh.pos_base;  // normals share vertex ids with positions
+    v3 n1 = xyz(S.nrm[e.x + b]), n2 = xyz(S.nrm[e.y + b]), n3 = xyz(S.nrm[e.z + b]);
+    if (sh.kind == KIND_TRI) return transform_normal(f, normalize(interp_tri(n1, n2, n3, uv)));
+    return transform_normal(f, normalize(interp_quad(n1, n2, n3, xyz(S.nrm[e.w + b]), uv)));
+}
+// eval_texcoord (src/scene.jl:753-788)
+__device__ __forceinline__ v2 eval_texcoord(const DScene& S, const DShape& sh, const int4& e, v2 uv) {
+    if (sh.tc_base < 0) return uv;
+    const int b = sh.tc_base - sh.pos_base;
+    float2 t1 = S.tc[e.x + b], t2 = S.tc[e.y + b], t3 = S.tc[e.z + b];
+    if (sh.kind == KIND_TRI) return interp_tri(V2(t1.x, t1.y), V2(t2.x, t2.y), V2(t3.x, t3.y), uv);
+    float2 t4 = S.tc[e.w + b];
+    return interp_quad(V2(t1.x, t1.y), V2(t2.x, t2.y), V2(t3.x, t3.y), V2(t4.x, t4.y), uv);
+}
+// eval_color (src/scene.jl:690-720)
+__device__ __forceinline__ v4 eval_color(const DScene& S, const DShape& sh, const int4& e, v2 uv) {
+    if (sh.col_base < 0) return V4(1, 1, 1, 1);
+    const int b = sh.col_base - sh.pos_base;
+    float4 c1 = S.col[e.x + b], c2 = S.col[e.y + b], c3 = S.col[e.z + b];
+    v4 a = V4(c1.x, c1.y, c1.z, c1.w), bb = V4(c2.x, c2.y, c2.z, c2.w), c = V4(c3.x, c3.y, c3.z, c3.w);
+    if (sh.kind == KIND_TRI) return interp_tri(a, bb, c, uv);
+    float4 c4 = S.col[e.w + b];
+    return interp_quad(a, bb, c, V4(c4.x, c4.y, c4.z, c4.w), uv);
+}
+// lookup_texture (src/scene.jl:836-849): 8-bit texels decode through exact host-built LUTs
+__device__ __forceinline__ v4 lookup_texture(const DScene& S, const DTexture& t, int i, int j, bool as_linear) {
+    long long k = t.offset + (long long)j * t.width + i;
+    if (t.is_float) {
+        float4 c = S.texf[k];
+        return V4(c.x, c.y, c.z, c.w);
+    }
+    uchar4 b = S.texb[k];
+    const float* lut = (as_linear && !t.linear) ? S.srgb_lut : S.byte_lut;
+    return V4(lut[b.x], lut[b.y], lut[b.z], S.byte_lut[b.w]);
+}
+// mod1(x, 1.0f0) (Julia base: mod via rem, then 0 -> 1)
+__device__ __forceinline__ float jl_mod1(float x) {
+    float r = __builtin_fmodf(x, 1.0f);
+    float m = r == 0 ? __builtin_copysignf(r, 1.0f) : (r < 0 ? r + 1.0f : r);
+    return m == 0 ? 1.0f : m;
+}
+// eval_texture (src/scene.jl:790-834): bilinear, wrap
+__device__ __forceinline__ v4 eval_texture(const DScene& S, int tex, v2 uv, bool as_linear) {
+    if (tex < 0) return V4(1, 1, 1, 1);
+    const DTexture t = S.textures[tex];
+    if (t.width == 0 || t.height == 0) return V4(0, 0, 0, 0);
+    float s = jl_mod1(uv.x) * (float)t.width;
+    if (s < 0) s += (float)t.width;
+    float tt = jl_mod1(uv.y) * (float)t.height;
+    if (tt < 0) tt += (float)t.height;
+    int i = jl_clampi((int)__builtin_truncf(s), 0, t.width - 1);
+    int j = jl_clampi((int)__builtin_truncf(tt), 0, t.height - 1);
+    int ii = (i + 1) % t.width, jj = (j + 1) % t.height;
+    float u = s - (float)i, v = tt - (float)j;
+    v4 a = (lookup_texture(S, t, i, j, as_linear) * (1 - u)) * (1 - v);
+    v4 b = (lookup_texture(S, t, i, jj, as_linear) * (1 - u)) * v;
+    v4 c = (lookup_texture(S, t, ii, j, as_linear) * u) * (1 - v);
+    v4 d = (lookup_texture(S, t, ii, jj, as_linear) * u) * v;
+    return ((a + b) + c) + d;
+}
+// eval_normalmap (src/scene.jl:722-751) with eval_element_tangents (:851-891)
+__device__ __noinline__ v3 eval_normalmap(const DScene& S, const DShape& sh, const int4& e, const fr3& f,
+                                          const DMaterial& m, v2 uv) {
+    v3 normal = eval_normal(S, sh, e, f, uv);
+    v2 texcoord = eval_texcoord(S, sh, e, uv);
+    v4 t4 = eval_texture(S, m.normal_tex, texcoord, false);
+    v3 nm = V3(t4.x * 2 - 1, t4.y * 2 - 1, t4.z * 2 - 1);
+    v3 tu = V3(0, 0, 0), tv = V3(0, 0, 0);
+    if (sh.tc_base >= 0) {
+        const int b = sh.tc_base - sh.pos_base;
+        float2 a1 = S.tc[e.x + b], a2 = S.tc[e.y + b];
+        if (sh.kind == KIND_TRI) {
+            float2 a3 = S.tc[e.z + b];
+            triangle_tangents_fromuv(xyz(S.pos[e.x]), xyz(S.pos[e.y]), xyz(S.pos[e.z]), V2(a1.x, a1.y),
+                                     V2(a2.x, a2.y), V2(a3.x, a3.y), tu, tv);
+        } else {  // quad_tangents_fromuv at current_uv = (0, 0): triangle (p1, p2, p4)
+            float2 a4 = S.tc[e.w + b];
+            triangle_tangents_fromuv(xyz(S.pos[e.x]), xyz(S.pos[e.y]), xyz(S.pos[e.w]), V2(a1.x, a1.y),
+                                     V2(a2.x, a2.y), V2(a4.x, a4.y), tu, tv);
+        }
+        tu = transform_direction(f, tu);
+        tv = transform_direction(f, tv);
+    }
+    v3 f1 = normalize(tu - normal * dot(tu, normal));  // orthonormalize(frame[1], frame[3])
+    v3 f2 = normalize(cross(normal, tu));
+    bool flip_v = dot(f2, tv) < 0;
+    nm = V3(nm.x, nm.y * (flip_v ? 1.0f : -1.0f), nm.z);
+    fr3 fr{f1, f2, normal, V3(0, 0, 0)};
+    return transform_normal(fr, nm);
+}
+
+struct Shading {
+    v3 position, normal;
+    MatPoint mat;
+};
+
+// eval_shading_position + eval_shading_normal + eval_material (src/scene.jl:416-673)
+__device__ __forceinline__ void eval_shading(const DScene& S, int inst, int elem, v2 uv, v3 outgoing, Shading& out) {
+    const DInstShade is = S.inst_shade[inst];
+    const DShape sh = S.shapes[is.shape];
+    const int4 e = S.elems[sh.idx_base + elem];
+    const fr3 f = frame_from(is.f0, is.f1, is.f2);
+    const DMaterial& m = S.materials[is.material];
+    v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
+    v3 p4 = sh.kind == KIND_QUAD ? xyz(S.pos[e.w]) : p3;
+    // position
+    out.position = sh.kind == KIND_TRI ? transform_point(f, interp_tri(p1, p2, p3, uv))
+                                       : transform_point(f, interp_quad(p1, p2, p3, p4, uv));
+    // shading normal
+    v3 normal;
+    if (m.normal_tex >= 0) {
+        normal = eval_normalmap(S, sh, e, f, m, uv);
+    } else if (sh.nrm_base < 0) {
+        normal = sh.kind == KIND_TRI ? transform_normal(f, triangle_normal(p1, p2, p3))
+                                     : transform_normal(f, quad_normal(p1, p2, p3, p4));
+    } else {
+        normal = eval_normal(S, sh, e, f, uv);
+    }
+    if (m.type != M_REFRACTIVE) normal = dot(normal, outgoing) >= 0 ? normal : -normal;
+    out.normal = normal;
+    // material point
+    MatPoint& p = out.mat;
+    v2 texcoord = eval_texcoord(S, sh, e, uv);
+    v4 emission_tex = eval_texture(S, m.emission_tex, texcoord, true);
+    v4 color_shp = eval_color(S, sh, e, uv);
+    v4 color_tex = eval_texture(S, m.color_tex, texcoord, true);
+    v4 roughness_tex = eval_texture(S, m.roughness_tex, texcoord, false);
+    v4 scattering_tex = eval_texture(S, m.scattering_tex, texcoord, true);
+    p.type = m.type;
+    p.emission = V3(m.emission[0], m.emission[1], m.emission[2]) * xyz(emission_tex);
+    p.color = (V3(m.color[0], m.color[1], m.color[2]) * xyz(color_tex)) * xyz(color_shp);
+    p.opacity = m.opacity * color_tex.w * color_shp.w;
+    p.metallic = m.metallic * roughness_tex.z;
+    float roughness = m.roughness * roughness_tex.y;
+    roughness = roughness * roughness;
+    p.ior = m.ior;
+    p.scattering = V3(m.scattering[0], m.scattering[1], m.scattering[2]) * xyz(scattering_tex);
+    p.scanisotropy = m.scanisotropy;
+    p.trdepth = m.trdepth;
+    if (m.type == M_REFRACTIVE || m.type == M_VOLUMETRIC || m.type == M_SUBSURFACE) {
+        p.density = V3(-jl_log(jl_clamp(p.color.x, 0.0001f, 1.0f)) / p.trdepth,
+                       -jl_log(jl_clamp(p.color.y, 0.0001f, 1.0f)) / p.trdepth,
+                       -jl_log(jl_clamp(p.color.z, 0.0001f, 1.0f)) / p.trdepth);
+    } else {
+        p.density = V3(0, 0, 0);
+    }
+    if (m.type == M_MATTE || m.type == M_GLTFPBR || m.type == M_GLOSSY) roughness = jl_clamp(roughness, min_roughness, 1.0f);
+    else if (m.type == M_VOLUMETRIC) roughness = 0.0f;
+    else if (roughness < min_roughness) roughness = 0.0f;
+    p.roughness = roughness;
+}
+
+// eval_environment (src/scene.jl:893-914)
+__device__ __noinline__ v3 eval_environment(const DScene& S, v3 direction) {
+    v3 emission = V3(0, 0, 0);
+    for (int k = 0; k < S.nenvs; k++) {
+        const DEnv& env = S.envs[k];
+        v3 wl = transform_direction(frame_from(env.inv), direction);
+        v2 tc = V2(jl_atan2(wl.z, wl.x) / (2.0f * pif), jl_acos(jl_clamp(wl.y, -1.0f, 1.0f)) / pif);
+        if (tc.x < 0.0f) tc.x = tc.x + 1.0f;
+        v4 t = eval_texture(S, env.tex, tc, false);
+        emission = emission + V3(env.emission[0], env.emission[1], env.emission[2]) * xyz(t);
+    }
+    return emission;
+}
+
+// ============================================================================ traversal (src/bvh.jl)
+// Unified per-lane stack in LDS, entry = type << 30 | index. Layout stack[k * BLOCK + lane]:
+// every lane owns one bank (conflict-free ds_read/write_b32 whatever the per-lane depth).
+constexpr int BLOCK = 256;
+constexpr unsigned T_TLAS = 0u, T_INST = 1u, T_BLAS = 2u;
+constexpr unsigned IDX_MASK = (1u << 30) - 1;
+
+struct Hit {
+    int inst, elem;
+    float u, v, t;
+    bool hit;
+};
+struct Counters {
+    unsigned rays, light_queries, nodes, instances, prims, shades, paths;
+};
+
+// One traversal loop for intersect_scene_bvh (root = TLAS node 0) and intersect_instance_bvh
+// (root = one instance entry). Closest hit; a primitive with t == tmax replaces the current hit,
+// exactly as the reference's `t > ray.tmax -> reject` test in the reference's visit order.
+__device__ __forceinline__ Hit traverse(const DScene& S, v3 wo, v3 wd, unsigned root, int* stack, Counters& cnt) {
+    Hit h{-1, -1, 0, 0, 0, false};
+    float tmax = __builtin_inff();
+    const float tmin = ray_eps;
+    const v3 wdinv = V3(1 / wd.x, 1 / wd.y, 1 / wd.z);
+    v3 lo = wo, ld = wd, ldinv = wdinv;
+    int cur_inst = -1, cur_kind = KIND_TRI;
+    int sp = 0;
+    stack[0] = (int)root;
+    sp = 1;
+    while (sp > 0) {
+        sp--;
+        const unsigned e = (unsigned)stack[sp * BLOCK];
+        const unsigned type = e >> 30, idx = e & IDX_MASK;
+        if (type == T_INST) {
+            // instance visit: inverse(frame, true) precomputed on the host (src/bvh.jl:345,502)
+            const DInstTrav it = S.inst_trav[idx];
+            cnt.instances++;
+            const fr3 inv = frame_from(it.i0, it.i1, it.i2);
+            lo = transform_point(inv, wo);
+            ld = transform_vector(inv, wd);
+            ldinv = V3(1 / ld.x, 1 / ld.y, 1 / ld.z);
+            cur_inst = (int)idx;
+            cur_kind = it.kind;
+            stack[sp * BLOCK] = (int)((T_BLAS << 30) | (unsigned)it.blas_root);
+            sp++;
+            continue;
+        }
+        const bool blas = type == T_BLAS;
+        const DNode nd = blas ? S.blas_nodes[idx] : S.tlas_nodes[idx];
+        cnt.nodes++;
+        const v3 o = blas ? lo : wo;
+        const v3 dv = blas ? ldinv : wdinv;
+        if (!intersect_bbox(o, dv, tmin, tmax, nd.a, nd.b)) continue;
+        const unsigned meta = __float_as_uint(nd.b.w);
+        const int start = __float_as_int(nd.a.w);
+        const int num = (int)(meta & 0xffffu);
+        if (meta >> 24) {  // internal: children start, start+1; far child first for d[axis] >= 0
+            const int axis = (int)((meta >> 16) & 0xffu);
+            const v3 d = blas ? ld : wd;
+            const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+            const unsigned tag = type << 30;
+            const int first = da < 0 ? start + 1 : start;
+            const int second = da < 0 ? start : start + 1;
+            stack[sp * BLOCK] = (int)(tag | (unsigned)first);
+            stack[(sp + 1) * BLOCK] = (int)(tag | (unsigned)second);
+            sp += 2;
+        } else if (!blas) {  // TLAS leaf: instances in order start .. start+num-1
+            for (int k = num - 1; k >= 0; k--) {
+                stack[sp * BLOCK] = (int)((T_INST << 30) | (unsigned)S.tlas_prims[start + k]);
+                sp++;
+            }
+        } else if (cur_kind == KIND_TRI) {
+            for (int k = 0; k < num; k++) {
+                const float4* r = S.prims + 3 * (start + k);
+                const float4 a = r[0], b = r[1], c = r[2];
+                cnt.prims++;
+                PrimHit p = intersect_triangle(lo, ld, tmin, tmax, xyz(a), xyz(b), xyz(c));
+                if (p.hit) {
+                    h = Hit{cur_inst, __float_as_int(a.w), p.u, p.v, p.t, true};
+                    tmax = p.t;
+                }
+            }
+        } else {
+            for (int k = 0; k < num; k++) {
+                const float4* r = S.prims + 4 * (start + k);
+                const float4 a = r[0], b = r[1], c = r[2], d = r[3];
+                cnt.prims++;
+                PrimHit p = intersect_quad(lo, ld, tmin, tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
+                if (p.hit) {
+                    h = Hit{cur_inst, __float_as_int(a.w), p.u, p.v, p.t, true};
+                    tmax = p.t;
+                }
+            }
+        }
+    }
+    return h;
+}
+
+// ============================================================================ lights (src/trace.jl)
+// sample_lights (src/trace.jl:968-1008)
+__device__ __forceinline__ v3 sample_lights(const DScene& S, v3 position, float rl, float rel, v2 ruv) {
+    const int light_id = sample_uniform(S.nlights, rl);
+    const DLight l = S.lights[light_id - 1];
+    const float* cdf = S.cdf + l.cdf_offset;
+    if (l.instance >= 0) {
+        const int element = sample_discrete(cdf, l.ncdf, rel);
+        const DShape sh = S.shapes[S.inst_shade[l.instance].shape];
+        v2 uv = sh.kind == KIND_TRI ? sample_triangle(ruv) : ruv;
+        v3 lposition = eval_position(S, l.instance, element - 1, uv);
+        return normalize(lposition - position);
+    }
+    if (l.environment >= 0) {
+        const DEnv& env = S.envs[l.environment];
+        const DTexture t = S.textures[env.tex];
+        const int idx = sample_discrete(cdf, l.ncdf, rel);  // 1-based, used as-is (:990-993)
+        float u = ((float)(idx % t.width) + 0.5f) / (float)t.width;
+        float v = (float)((((double)idx / (double)t.width) + 0.5) / (double)t.height);
+        float su, cu, sv, cv;
+        jl_sincos(u * 2 * pif, &su, &cu);
+        jl_sincos(v * pif, &sv, &cv);
+        return transform_direction(frame_from(env.frame), V3(cu * sv, cv, su * sv));
+    }
+    return V3(0, 0, 0);
+}
+// sample_lights_pdf (src/trace.jl:1010-1084)
+__device__ __forceinline__ float sample_lights_pdf(const DScene& S, v3 position, v3 direction, int* stack, Counters& cnt) {
+    float pdf = 0.0f;
+    for (int li = 0; li < S.nlights; li++) {
+        const DLight l = S.lights[li];
+        const float* cdf = S.cdf + l.cdf_offset;
+        if (l.instance >= 0) {
+            float lpdf = 0.0f;
+            v3 next_position = position;
+            const float area = cdf[l.ncdf - 1];
+            for (int bounce = 0; bounce < 100; bounce++) {
+                cnt.light_queries++;
+                Hit h = traverse(S, next_position, direction, (T_INST << 30) | (unsigned)l.instance, stack, cnt);
+                if (!h.hit) break;
+                v3 lposition = eval_position(S, l.instance, h.elem, V2(h.u, h.v));
+                v3 lnormal = eval_element_normal(S, l.instance, h.elem);
+                v3 dd = lposition - position;
+                lpdf += dot(dd, dd) / (__builtin_fabsf(dot(lnormal, direction)) * area);
+                next_position = lposition + direction * 0.001f;
+            }
+            pdf += lpdf;
+        } else if (l.environment >= 0) {
+            const DEnv& env = S.envs[l.environment];
+            const DTexture t = S.textures[env.tex];
+            v3 wl = transform_direction(frame_from(env.inv), direction);
+            v2 tc = V2(jl_atan2(wl.z, wl.x) / (2 * pif), jl_acos(jl_clamp(wl.y, -1.0f, 1.0f)) / pif);
+            if (tc.x < 0) tc.x = tc.x + 1;
+            int i = jl_clampi((int)__builtin_truncf(tc.x * (float)t.width), 0, t.width - 1);
+            int j = jl_clampi((int)__builtin_truncf(tc.y * (float)t.height), 0, t.height - 1);
+            float prob = sample_discrete_pdf(cdf, j * t.width + i + 1) / cdf[l.ncdf - 1];
+            float angle = (2 * pif / (float)t.width) * (pif / (float)t.height) *
+                          jl_sin(pif * ((float)j + 0.5f) / (float)t.height);
+            pdf += prob / angle;
+        }
+    }
+    pdf *= sample_uniform_pdf(S.nlights);
+    return pdf;
+}
+
+// ============================================================================ integrator
+struct Path {
+    v3 o, d;      // current ray (tmin = ray_eps, tmax = inf at each query)
+    v3 cam_d;     // camera ray direction (the normal AOV's fallback, src/trace.jl:642,647)
+    v3 radiance, weight;
+    v3 hit_albedo, hit_normal;
+    Volume vol;
+    float max_roughness;
+    int bounce, opbounce, cur_volume;
+    bool hit;
+    Rng rng;
+};
+
+// eval_camera (src/scene.jl:372-411)
+__device__ __forceinline__ void eval_camera(const DCamera& cam, v2 image_uv, v2 lens_uv, v3& ro, v3& rd) {
+    const fr3 frame = frame_from(cam.frame);
+    v2 film = cam.aspect >= 1 ? V2(cam.film, cam.film / cam.aspect) : V2(cam.film * cam.aspect, cam.film);
+    if (!cam.orthographic) {
+        v3 q = V3(film.x * (0.5f - image_uv.x), film.y * (image_uv.y - 0.5f), cam.lens);
+        v3 dc = -normalize(q);
+        v3 e = V3(lens_uv.x * cam.aperture / 2, lens_uv.y * cam.aperture / 2, 0);
+        v3 p = (dc * cam.focus) / __builtin_fabsf(dc.z);
+        v3 d = normalize(p - e);
+        ro = transform_point(frame, e);
+        rd = transform_direction(frame, d);
+    } else {
+        float scale = 1 / cam.lens;
+        v3 q = V3(film.x * (0.5f - image_uv.x) * scale, film.y * (image_uv.y - 0.5f) * scale, cam.lens);
+        v3 e = V3(-q.x, -q.y, 0) + V3(lens_uv.x * cam.aperture / 2, lens_uv.y * cam.aperture / 2, 0);
+        v3 p = V3(-q.x, -q.y, -cam.focus);
+        v3 d = normalize(p - e);
+        ro = transform_point(frame, e);
+        rd = transform_direction(frame, d);
+    }
+}
+
+// trace_sample prologue (src/trace.jl:597-608): 4 draws, camera ray (sample_camera :651-674)
+__device__ __forceinline__ void start_path(const DParams& P, int i, int j, int pixel, int sample, Path& st) {
+    st.rng = rng_init(P.seed, pixel, sample);
+    v2 puv = rand2f(st.rng);
+    v2 luv = rand2f(st.rng);
+    v2 uv;
+    if (!P.tentfilter) {
+        uv = V2(((float)i + puv.x) / (float)P.width, ((float)j + puv.y) / (float)P.height);
+    } else {
+        const float width = 2.0f, offset = 0.5f;
+        v2 fuv = V2(width * (puv.x < 0.5f ? __builtin_sqrtf(2 * puv.x) - 1 : 1 - __builtin_sqrtf(2 - 2 * puv.x)) + offset,
+                    width * (puv.y < 0.5f ? __builtin_sqrtf(2 * puv.y) - 1 : 1 - __builtin_sqrtf(2 - 2 * puv.y)) + offset);
+        uv = V2(((float)i + fuv.x) / (float)P.width, ((float)j + fuv.y) / (float)P.height);
+    }
+    eval_camera(P.cam, uv, sample_disk(luv), st.o, st.d);
+    st.cam_d = st.d;
+    st.radiance = V3(0, 0, 0);
+    st.weight = V3(1, 1, 1);
+    st.hit_albedo = V3(0, 0, 0);
+    st.hit_normal = V3(0, 0, 0);
+    st.vol = Volume{V3(0, 0, 0), V3(0, 0, 0), 0.0f};
+    st.max_roughness = 0.0f;
+    st.bounce = -1;
+    st.opbounce = 0;
+    st.cur_volume = 0;
+    st.hit = false;
+}
+
+// One iteration of trace_path's bounce loop (src/trace.jl:296-466). Returns true when the path
+// is finished (the reference's `break` or the loop condition failing).
+__device__ __forceinline__ bool step_path(const DScene& S, const DParams& P, Path& st, int* stack, Counters& cnt) {
+    if (st.bounce >= P.bounces) return true;
+    st.bounce += 1;
+    cnt.rays++;
+    Hit isec = traverse(S, st.o, st.d, T_TLAS << 30, stack, cnt);
+    if (!isec.hit) {
+        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment(S, st.d);
+        return true;
+    }
+    bool in_volume = false;
+    if (st.cur_volume != 0) {  // :307-326
+        float rl = rand1f(st.rng), rd = rand1f(st.rng);
+        float distance = sample_transmittance(st.vol.density, isec.t, rl, rd);
+        v3 tr = eval_transmittance(st.vol.density, distance);
+        float tp = sample_transmittance_pdf(st.vol.density, distance, isec.t);
+        st.weight = (st.weight * tr) / tp;
+        in_volume = distance < isec.t;
+        isec.t = distance;
+    }
+    v3 incoming;
+    if (!in_volume) {  // surface (:328-423)
+        v3 outgoing = -st.d;
+        Shading sh;
+        eval_shading(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
+        cnt.shades++;
+        if (P.nocaustics) {
+            st.max_roughness = jl_max(sh.mat.roughness, st.max_roughness);
+            sh.mat.roughness = st.max_roughness;
+        }
+        if (sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
+            if (st.opbounce > 128) return true;
+            st.opbounce += 1;
+            st.o = sh.position + st.d * 0.01f;
+            st.bounce -= 1;
+            return false;
+        }
+        if (st.bounce == 0) {
+            st.hit = true;
+            st.hit_albedo = sh.mat.color;
+            st.hit_normal = sh.normal;
+        }
+        st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
+        if (!is_delta(sh.mat)) {
+            if (rand1f(st.rng) < 0.5f) {
+                float rnl = rand1f(st.rng);
+                v2 rn = rand2f(st.rng);
+                incoming = sample_bsdfcos(sh.mat, sh.normal, outgoing, rnl, rn);
+            } else {
+                float rl = rand1f(st.rng), rel = rand1f(st.rng);
+                v2 ruv = rand2f(st.rng);
+                incoming = sample_lights(S, sh.position, rl, rel, ruv);
+            }
+            if (is_zero(incoming)) return true;
+            v3 f = eval_bsdfcos(sh.mat, sh.normal, outgoing, incoming);
+            float pb = sample_bsdfcos_pdf(sh.mat, sh.normal, outgoing, incoming);
+            float pl = sample_lights_pdf(S, sh.position, incoming, stack, cnt);
+            st.weight = (st.weight * f) / (0.5f * pb + 0.5f * pl);
+        } else {
+            float rnl = rand1f(st.rng);
+            incoming = sample_delta(sh.mat, sh.normal, outgoing, rnl);
+            v3 f = eval_delta(sh.mat, sh.normal, outgoing, incoming);
+            float pd = sample_delta_pdf(sh.mat, sh.normal, outgoing, incoming);
+            st.weight = (st.weight * f) / pd;
+        }
+        const int mtype = S.inst_shade[isec.inst].mat_type;  // is_volumetric(scene, instance)
+        if ((mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE) &&
+            dot(sh.normal, outgoing) * dot(sh.normal, incoming) < 0) {
+            if (st.cur_volume == 0) {
+                // eval_material again (without the nocaustics override): only the volume fields
+                st.cur_volume += 1;
+                st.vol.density = sh.mat.density;
+                st.vol.scattering = sh.mat.scattering;
+                st.vol.scanisotropy = sh.mat.scanisotropy;
+            } else {
+                st.cur_volume -= 1;
+            }
+        }
+        st.o = sh.position;
+        st.d = incoming;
+    } else {  // volume scattering (:424-453)
+        v3 outgoing = -st.d;
+        v3 position = st.o + st.d * isec.t;
+        if (rand1f(st.rng) < 0.5f) {
+            rand1f(st.rng);  // rnl: drawn, unused by sample_scattering
+            v2 rn = rand2f(st.rng);
+            incoming = sample_scattering(st.vol, outgoing, rn);
+        } else {
+            float rl = rand1f(st.rng), rel = rand1f(st.rng);
+            v2 ruv = rand2f(st.rng);
+            incoming = sample_lights(S, position, rl, rel, ruv);
+        }
+        if (is_zero(incoming)) return true;
+        v3 f = eval_scattering(st.vol, outgoing, incoming);
+        float ps = sample_scattering_pdf(st.vol, outgoing, incoming);
+        float pl = sample_lights_pdf(S, position, incoming, stack, cnt);
+        st.weight = (st.weight * f) / (0.5f * ps + 0.5f * pl);
+        st.o = position;
+        st.d = incoming;
+    }
+    if (is_zero(st.weight) || !all_finite(st.weight)) return true;
+    if (st.bounce > 3) {  // Russian roulette (:459-465)
+        float rr_prob = jl_min(0.99f, max3(st.weight));
+        if (rand1f(st.rng) >= rr_prob) return true;
+        st.weight = st.weight * (1 / rr_prob);
+    }
+    return false;
+}
+
+// One iteration of trace_naive's bounce loop (src/trace.jl:488-570).
+__device__ __forceinline__ bool step_naive(const DScene& S, const DParams& P, Path& st, int* stack, Counters& cnt) {
+    if (st.bounce >= P.bounces) return true;
+    st.bounce += 1;
+    cnt.rays++;
+    Hit isec = traverse(S, st.o, st.d, T_TLAS << 30, stack, cnt);
+    if (!isec.hit) {
+        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment(S, st.d);
+        return true;
+    }
+    v3 outgoing = -st.d;
+    Shading sh;
+    eval_shading(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
+    cnt.shades++;
+    if (sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
+        if (st.opbounce > 128) return true;
+        st.opbounce += 1;
+        st.o = sh.position + st.d * 0.01f;
+        st.bounce -= 1;
+        return false;
+    }
+    if (st.bounce == 0) {
+        st.hit = true;
+        st.hit_albedo = sh.mat.color;
+        st.hit_normal = sh.normal;
+    }
+    st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
+    v3 incoming;
+    if (sh.mat.roughness != 0) {
+        float rnl = rand1f(st.rng);
+        v2 rn = rand2f(st.rng);
+        incoming = sample_bsdfcos(sh.mat, sh.normal, outgoing, rnl, rn);
+        if (is_zero(incoming)) return true;
+        v3 f = eval_bsdfcos(sh.mat, sh.normal, outgoing, incoming);
+        float p = sample_bsdfcos_pdf(sh.mat, sh.normal, outgoing, incoming);
+        st.weight = (st.weight * f) / p;
+    } else {
+        float rnl = rand1f(st.rng);
+        incoming = sample_delta(sh.mat, sh.normal, outgoing, rnl);
+        if (is_zero(incoming)) return true;
+        v3 f = eval_delta(sh.mat, sh.normal, outgoing, incoming);
+        float p = sample_delta_pdf(sh.mat, sh.normal, outgoing, incoming);
+        st.weight = (st.weight * f) / p;
+    }
+    if (is_zero(st.weight) || !all_finite(st.weight)) return true;
+    if (st.bounce > 3) {
+        float rr_prob = jl_min(0.99f, max3(st.weight));
+        if (rand1f(st.rng) >= rr_prob) return true;
+        st.weight = st.weight * (1 / rr_prob);
+    }
+    st.o = sh.position;
+    st.d = incoming;
+    return false;
+}
+
+struct DAccum {
+    float4* image;
+    float4* albedo;
+    float4* normal;
+    long long* hits;
+    unsigned long long* counters;  // 7 x u64: paths rays light_queries nodes instances prims shades
+};
+
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
+// 16x16-pixel workgroups; regenerates paths until the lane's samples are done.
+template <int SAMPLER, int STACK>
+__global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
+    __shared__ int lds_stack[STACK * BLOCK];
+    int* stack = lds_stack + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int j = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    if (i < P.width && j < P.height && s_begin < s_end) {
+        const int pixel = j * P.width + i;
+        float4 img = A.image[pixel], alb = A.albedo[pixel], nrm = A.normal[pixel];
+        long long hits = A.hits[pixel];
+        int sample = s_begin;
+        Path st;
+        start_path(P, i, j, pixel, sample, st);
+        for (;;) {
+            const bool done = SAMPLER == 2 ? step_naive(S, P, st, stack, cnt) : step_path(S, P, st, stack, cnt);
+            if (!done) continue;
+            // trace_sample epilogue (src/trace.jl:625-648)
+            cnt.paths++;
+            v3 radiance = st.radiance;
+            if (!all_finite(radiance)) radiance = V3(0, 0, 0);
+            const float mr = max3(radiance);
+            if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
+            const float w = 1.0f / (float)(sample - P.first + 1);
+            const float omw = 1 - w;
+            v4 target;
+            v3 ta, tn;
+            if (st.hit) {
+                target = V4(radiance.x, radiance.y, radiance.z, 1);
+                ta = st.hit_albedo;
+                tn = st.hit_normal;
+                hits += 1;
+            } else if (!P.envhidden && S.nenvs != 0) {
+                target = V4(radiance.x, radiance.y, radiance.z, 1);
+                ta = V3(1, 1, 1);
+                tn = -st.cam_d;
+                hits += 1;
+            } else {
+                target = V4(0, 0, 0, 0);
+                ta = V3(0, 0, 0);
+                tn = -st.cam_d;
+            }
+            img = make_float4(img.x * omw + target.x * w, img.y * omw + target.y * w, img.z * omw + target.z * w,
+                              img.w * omw + target.w * w);
+            alb = make_float4(alb.x * omw + ta.x * w, alb.y * omw + ta.y * w, alb.z * omw + ta.z * w, 0.0f);
+            nrm = make_float4(nrm.x * omw + tn.x * w, nrm.y * omw + tn.y * w, nrm.z * omw + tn.z * w, 0.0f);
+            if (++sample >= s_end) break;
+            start_path(P, i, j, pixel, sample, st);
+        }
+        A.image[pixel] = img;
+        A.albedo[pixel] = alb;
+        A.normal[pixel] = nrm;
+        A.hits[pixel] = hits;
+    }
+    // one atomic per counter per wave
+    unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims, cnt.shades};
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        unsigned s = wave_sum(v[k]);
+        if (lane == 0 && s) atomicAdd(&A.counters[k], (unsigned long long)s);
+    }
+}
+
+template <int SAMPLER, int STACK>
+hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st) {
+    dim3 grid((P.width + 15) / 16, (P.height + 15) / 16);
+    hipLaunchKernelGGL((trace_kernel<SAMPLER, STACK>), grid, dim3(BLOCK), 0, st, S, P, s0, s1, A);
+    return hipGetLastError();
+}
+
+template <int SAMPLER>
+hipError_t launch_s(int stack, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st) {
+    if (stack <= 16) return launch_t<SAMPLER, 16>(S, P, s0, s1, A, st);
+    if (stack <= 32) return launch_t<SAMPLER, 32>(S, P, s0, s1, A, st);
+    if (stack <= 64) return launch_t<SAMPLER, 64>(S, P, s0, s1, A, st);
+    return launch_t<SAMPLER, 128>(S, P, s0, s1, A, st);
+}
+
+}  // namespace
+
+// ============================================================================ C-ABI context
+struct jt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    DScene S{};
+    DParams P{};
+    DAccum A{};
+    std::vector<void*> allocations;
+    int width = 0, height = 0;
+    int total_samples = 0, batch = 1, sampler = 1, stack = 16;
+    int first = -1, next = 0;  // running-mean origin and next expected sample
+    unsigned long long launches = 0;
+    double kernel_ms = 0;
+};
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+    return jt::fail(JT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class T>
+int upload(jt_ctx* c, const std::vector<T>& host, const T** dptr) {
+    size_t bytes = std::max<size_t>(sizeof(T), host.size() * sizeof(T));
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return jt::fail(JT_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    c->allocations.push_back(p);
+    if (!host.empty()) {
+        e = hipMemcpy(p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+    }
+    *dptr = (const T*)p;
+    return JT_OK;
+}
+
+int tree_depth(const jt_bvh_tree& t) {
+    if (t.nnodes == 0) return 0;
+    std::vector<std::pair<int, int>> st{{0, 0}};
+    int depth = 0;
+    while (!st.empty()) {
+        auto [n, d] = st.back();
+        st.pop_back();
+        depth = std::max(depth, d);
+        const jt_bvh_node& nd = t.nodes[n];
+        if (nd.internal) {
+            st.push_back({nd.start, d + 1});
+            st.push_back({nd.start + 1, d + 1});
+        }
+    }
+    return depth;
+}
+
+inline float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
+inline float as_f(int v) {
+    float f;
+    std::memcpy(&f, &v, 4);
+    return f;
+}
+inline float as_f(unsigned v) {
+    float f;
+    std::memcpy(&f, &v, 4);
+    return f;
+}
+DNode pack_node(const jt_bvh_node& n, int start) {
+    unsigned meta = (unsigned)(uint16_t)n.num | ((unsigned)(uint8_t)n.axis << 16) | ((unsigned)(n.internal ? 1 : 0) << 24);
+    return DNode{f4(n.bmin[0], n.bmin[1], n.bmin[2], as_f(start)), f4(n.bmax[0], n.bmax[1], n.bmax[2], as_f(meta))};
+}
+
+int check_tree(const jt_bvh_tree& t, int nprims_expected, const char* what) {
+    if (t.nprimitives != nprims_expected) return jt::fail(JT_ERR_INVALID, std::string(what) + ": primitive count mismatch");
+    for (int k = 0; k < t.nnodes; k++) {
+        const jt_bvh_node& n = t.nodes[k];
+        if (n.internal) {
+            if (n.start < 0 || n.start + 1 >= t.nnodes) return jt::fail(JT_ERR_INVALID, std::string(what) + ": bad child index");
+        } else if (n.start < 0 || n.num < 0 || n.start + n.num > t.nprimitives) {
+            return jt::fail(JT_ERR_INVALID, std::string(what) + ": bad leaf range");
+        }
+    }
+    for (int k = 0; k < t.nprimitives; k++)
+        if (t.primitives[k] < 0 || t.primitives[k] >= nprims_expected)
+            return jt::fail(JT_ERR_INVALID, std::string(what) + ": bad primitive id");
+    return JT_OK;
+}
+
+// srgb_to_rgb(byte_to_float(b)) (src/color.jl:12-23), the power evaluated in double
+void build_luts(std::vector<float>& srgb, std::vector<float>& bytes) {
+    srgb.resize(256);
+    bytes.resize(256);
+    for (int b = 0; b < 256; b++) {
+        float c = (float)b / 255.0f;
+        bytes[b] = c;
+        srgb[b] = c <= 0.04045f ? c / 12.92f : (float)std::pow((double)((c + 0.055f) / 1.055f), (double)2.4f);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int jt_device_count(int32_t* out) {
+    if (!out) return jt::fail(JT_ERR_INVALID, "out is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *out = 0;
+        return hip_fail(e, "hipGetDeviceCount");
+    }
+    *out = n;
+    return JT_OK;
+}
+
+void jt_destroy(jt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (void* p : c->allocations) (void)hipFree(p);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights, const jt_params* params,
+              jt_ctx** out) {
+    if (!out) return jt::fail(JT_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (!scene || !bvh || !lights || !params) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    if (params->camera < 0 || params->camera >= scene->ncameras) return jt::fail(JT_ERR_INVALID, "camera id out of range");
+    if (params->sampler != JT_SAMPLER_PATH && params->sampler != JT_SAMPLER_NAIVE)
+        return jt::fail(JT_ERR_INVALID, "sampler must be 1 (path) or 2 (naive)");
+    if (params->samples < 0 || params->bounces < 0 || params->batch < 1)
+        return jt::fail(JT_ERR_INVALID, "samples/bounces must be >= 0 and batch >= 1");
+    if (bvh->nshapes != scene->nshapes) return jt::fail(JT_ERR_INVALID, "bvh.nshapes != scene.nshapes");
+    // ------------------------------------------------------------- validate what the reference can shade
+    for (int s = 0; s < scene->nshapes; s++) {
+        const jt_shape& sh = scene->shapes[s];
+        if (sh.npoints > 0 || (sh.nlines > 0 && sh.ntriangles == 0 && sh.nquads == 0))
+            return jt::fail(JT_ERR_UNSUPPORTED, "shape " + std::to_string(s) +
+                                                    ": points/lines are not shaded by the reference (src/scene.jl:429,605)");
+        if (sh.ntriangles == 0 && sh.nquads == 0)
+            return jt::fail(JT_ERR_UNSUPPORTED, "shape " + std::to_string(s) + " has no triangles or quads");
+        if (sh.nnormals != 0 && sh.nnormals != sh.npositions)
+            return jt::fail(JT_ERR_INVALID, "shape " + std::to_string(s) + ": normals/positions length mismatch");
+        if (sh.ntexcoords != 0 && sh.ntexcoords != sh.npositions)
+            return jt::fail(JT_ERR_INVALID, "shape " + std::to_string(s) + ": texcoords/positions length mismatch");
+        if (sh.ncolors != 0 && sh.ncolors != sh.npositions)
+            return jt::fail(JT_ERR_INVALID, "shape " + std::to_string(s) + ": colors/positions length mismatch");
+        const int32_t* idx = sh.ntriangles ? sh.triangles : sh.quads;
+        long n = sh.ntriangles ? 3L * sh.ntriangles : 4L * sh.nquads;
+        for (long k = 0; k < n; k++)
+            if (idx[k] < 0 || idx[k] >= sh.npositions)
+                return jt::fail(JT_ERR_INVALID, "shape " + std::to_string(s) + ": vertex id out of range");
+    }
+    for (int k = 0; k < scene->ninstances; k++) {
+        const jt_instance& in = scene->instances[k];
+        if (in.shape < 0 || in.shape >= scene->nshapes || in.material < 0 || in.material >= scene->nmaterials)
+            return jt::fail(JT_ERR_INVALID, "instance " + std::to_string(k) + ": invalid shape/material id");
+        if (scene->materials[in.material].type == JT_GLTFPBR)
+            return jt::fail(JT_ERR_UNSUPPORTED, "instance " + std::to_string(k) +
+                                                    ": gltfpbr calls undefined functions in the reference (src/shading.jl:254-321)");
+    }
+    auto tex_ok = [&](int t) { return t >= -1 && t < scene->ntextures; };
+    for (int k = 0; k < scene->nmaterials; k++) {
+        const jt_material& m = scene->materials[k];
+        if (m.type < 0 || m.type > JT_GLTFPBR) return jt::fail(JT_ERR_INVALID, "material type out of range");
+        if (!tex_ok(m.emission_tex) || !tex_ok(m.color_tex) || !tex_ok(m.roughness_tex) || !tex_ok(m.scattering_tex) ||
+            !tex_ok(m.normal_tex))
+            return jt::fail(JT_ERR_INVALID, "material " + std::to_string(k) + ": texture id out of range");
+    }
+    for (int k = 0; k < scene->nenvironments; k++)
+        if (!tex_ok(scene->environments[k].emission_tex)) return jt::fail(JT_ERR_INVALID, "environment texture id out of range");
+    for (int k = 0; k < lights->nlights; k++) {
+        const jt_light& l = lights->lights[k];
+        if ((l.instance >= 0) == (l.environment >= 0) || l.ncdf <= 0 || !l.cdf)
+            return jt::fail(JT_ERR_INVALID, "light " + std::to_string(k) + ": malformed");
+        if (l.instance >= scene->ninstances || l.environment >= scene->nenvironments)
+            return jt::fail(JT_ERR_INVALID, "light " + std::to_string(k) + ": id out of range");
+        if (l.environment >= 0 && scene->environments[l.environment].emission_tex < 0)
+            return jt::fail(JT_ERR_UNSUPPORTED, "untextured environment light: sample_sphere is undefined (src/trace.jl:1003)");
+    }
+    int st = check_tree(bvh->tlas, scene->ninstances, "tlas");
+    if (st != JT_OK) return st;
+    int max_blas_depth = 0;
+    for (int s = 0; s < scene->nshapes; s++) {
+        const jt_shape& sh = scene->shapes[s];
+        st = check_tree(bvh->blas[s], sh.ntriangles ? sh.ntriangles : sh.nquads, "blas");
+        if (st != JT_OK) return st;
+        max_blas_depth = std::max(max_blas_depth, tree_depth(bvh->blas[s]));
+    }
+    const int tlas_depth = tree_depth(bvh->tlas);
+    // the reference's stacks hold bvhstacksize entries each; a DFS needs depth + 1
+    if (std::max(tlas_depth, max_blas_depth) + 1 > params->bvhstacksize)
+        return jt::fail(JT_ERR_STACK, "BVH deeper than --bvhstacksize (the reference throws BoundsError)");
+    const int need = tlas_depth + max_blas_depth + 6;  // unified stack bound
+    if (need > 128) return jt::fail(JT_ERR_UNSUPPORTED, "BVH too deep for the 128-entry LDS stack");
+
+    int32_t W = 0, H = 0;
+    st = jt_image_size(scene, params, &W, &H);
+    if (st != JT_OK) return st;
+
+    hipError_t e = hipSetDevice(params->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    jt_ctx* c = new jt_ctx();
+    c->device = params->device;
+    c->width = W;
+    c->height = H;
+    c->total_samples = params->samples;
+    c->batch = params->batch;
+    c->sampler = params->sampler;
+    c->stack = need;
+    auto bail = [&](int status) {
+        jt_destroy(c);
+        return status;
+    };
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail(hip_fail(e, "hipStreamCreate"));
+    if ((e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess)
+        return bail(hip_fail(e, "hipEventCreate"));
+
+    // ------------------------------------------------------------- flatten to the HBM layout
+    std::vector<DNode> tlas(std::max(0, bvh->tlas.nnodes));
+    for (int k = 0; k < bvh->tlas.nnodes; k++) tlas[k] = pack_node(bvh->tlas.nodes[k], bvh->tlas.nodes[k].start);
+    std::vector<int> tlas_prims(bvh->tlas.primitives, bvh->tlas.primitives + bvh->tlas.nprimitives);
+    std::vector<DNode> blas;
+    std::vector<float4> prims;
+    std::vector<DShape> shapes(scene->nshapes);
+    std::vector<float4> pos, nrm, col;
+    std::vector<float2> tc;
+    std::vector<int4> elems;
+    for (int s = 0; s < scene->nshapes; s++) {
+        const jt_shape& sh = scene->shapes[s];
+        const jt_bvh_tree& t = bvh->blas[s];
+        DShape& d = shapes[s];
+        d.kind = sh.ntriangles ? KIND_TRI : KIND_QUAD;
+        const int stride = d.kind == KIND_TRI ? 3 : 4;
+        d.blas_root = (int)blas.size();
+        d.prim_base = (int)(prims.size() / stride);  // in records
+        d.idx_base = (int)elems.size();
+        d.pos_base = (int)pos.size();
+        for (int v = 0; v < sh.npositions; v++) pos.push_back(f4(sh.positions[3 * v], sh.positions[3 * v + 1], sh.positions[3 * v + 2], 0));
+        d.nrm_base = -1;
+        d.tc_base = -1;
+        d.col_base = -1;
+        // per-vertex attribute arrays are padded to the positions' base so one vertex id serves all
+        if (sh.nnormals) {
+            while ((int)nrm.size() < d.pos_base) nrm.push_back(f4(0, 0, 0, 0));
+            d.nrm_base = (int)nrm.size();
+            for (int v = 0; v < sh.nnormals; v++) nrm.push_back(f4(sh.normals[3 * v], sh.normals[3 * v + 1], sh.normals[3 * v + 2], 0));
+        }
+        if (sh.ntexcoords) {
+            while ((int)tc.size() < d.pos_base) tc.push_back(make_float2(0, 0));
+            d.tc_base = (int)tc.size();
+            for (int v = 0; v < sh.ntexcoords; v++) tc.push_back(make_float2(sh.texcoords[2 * v], sh.texcoords[2 * v + 1]));
+        }
+        if (sh.ncolors) {
+            while ((int)col.size() < d.pos_base) col.push_back(f4(0, 0, 0, 0));
+            d.col_base = (int)col.size();
+            for (int v = 0; v < sh.ncolors; v++)
+                col.push_back(f4(sh.colors[4 * v], sh.colors[4 * v + 1], sh.colors[4 * v + 2], sh.colors[4 * v + 3]));
+        }
+        const int nel = d.kind == KIND_TRI ? sh.ntriangles : sh.nquads;
+        for (int k = 0; k < nel; k++) {
+            if (d.kind == KIND_TRI)
+                elems.push_back(make_int4(d.pos_base + sh.triangles[3 * k], d.pos_base + sh.triangles[3 * k + 1],
+                                          d.pos_base + sh.triangles[3 * k + 2], 0));
+            else
+                elems.push_back(make_int4(d.pos_base + sh.quads[4 * k], d.pos_base + sh.quads[4 * k + 1],
+                                          d.pos_base + sh.quads[4 * k + 2], d.pos_base + sh.quads[4 * k + 3]));
+        }
+        for (int k = 0; k < t.nnodes; k++) {
+            const jt_bvh_node& n = t.nodes[k];
+            blas.push_back(pack_node(n, n.internal ? d.blas_root + n.start : d.prim_base + n.start));
+        }
+        // primitive records in BVH leaf order (the reference reads positions through
+        // bvh.primitives[i]; the records hold the same floats, pre-gathered)
+        for (int k = 0; k < t.nprimitives; k++) {
+            const int el = t.primitives[k];
+            const int* v = d.kind == KIND_TRI ? &sh.triangles[3 * el] : &sh.quads[4 * el];
+            auto P3 = [&](int vi) { return f4(sh.positions[3 * vi], sh.positions[3 * vi + 1], sh.positions[3 * vi + 2], 0); };
+            float4 a = P3(v[0]), b = P3(v[1]), cc = P3(v[2]);
+            a.w = as_f(el);
+            prims.push_back(a);
+            prims.push_back(b);
+            prims.push_back(cc);
+            if (d.kind == KIND_QUAD) {
+                float4 dd = P3(v[3]);
+                const bool degenerate = cc.x == dd.x && cc.y == dd.y && cc.z == dd.z;  // p3 == p4
+                dd.w = degenerate ? 1.0f : 0.0f;
+                prims.push_back(dd);
+            }
+        }
+    }
+    std::vector<DInstTrav> itrav(scene->ninstances);
+    std::vector<DInstShade> ishade(scene->ninstances);
+    for (int k = 0; k < scene->ninstances; k++) {
+        const jt_instance& in = scene->instances[k];
+        jt::frame3 f = jt::load_frame(in.frame);
+        jt::frame3 inv = jt::inverse_frame(f, true);
+        float iv[12], fv[12];
+        jt::store_frame(inv, iv);
+        jt::store_frame(f, fv);
+        const DShape& d = shapes[in.shape];
+        itrav[k] = DInstTrav{f4(iv[0], iv[1], iv[2], iv[3]), f4(iv[4], iv[5], iv[6], iv[7]), f4(iv[8], iv[9], iv[10], iv[11]),
+                             in.shape, d.blas_root, d.kind, d.prim_base};
+        ishade[k] = DInstShade{f4(fv[0], fv[1], fv[2], fv[3]), f4(fv[4], fv[5], fv[6], fv[7]), f4(fv[8], fv[9], fv[10], fv[11]),
+                               in.material, in.shape, scene->materials[in.material].type, 0};
+    }
+    std::vector<DMaterial> mats(scene->nmaterials);
+    for (int k = 0; k < scene->nmaterials; k++) {
+        const jt_material& m = scene->materials[k];
+        DMaterial& d = mats[k];
+        std::memset(&d, 0, sizeof(d));
+        d.type = m.type;
+        d.emission_tex = m.emission_tex;
+        d.color_tex = m.color_tex;
+        d.roughness_tex = m.roughness_tex;
+        d.scattering_tex = m.scattering_tex;
+        d.normal_tex = m.normal_tex;
+        for (int q = 0; q < 3; q++) {
+            d.emission[q] = m.emission[q];
+            d.color[q] = m.color[q];
+            d.scattering[q] = m.scattering[q];
+        }
+        d.roughness = m.roughness;
+        d.metallic = m.metallic;
+        d.ior = m.ior;
+        d.scanisotropy = m.scanisotropy;
+        d.trdepth = m.trdepth;
+        d.opacity = m.opacity;
+    }
+    std::vector<DTexture> texs(scene->ntextures);
+    std::vector<uchar4> texb;
+    std::vector<float4> texf;
+    for (int k = 0; k < scene->ntextures; k++) {
+        const jt_texture& t = scene->textures[k];
+        DTexture& d = texs[k];
+        std::memset(&d, 0, sizeof(d));
+        d.width = t.width;
+        d.height = t.height;
+        d.linear = t.linear;
+        d.is_float = t.pixelsf != nullptr;
+        const size_t n = (size_t)t.width * (size_t)t.height;
+        if (d.is_float) {
+            d.offset = (long long)texf.size();
+            for (size_t q = 0; q < n; q++)
+                texf.push_back(f4(t.pixelsf[4 * q], t.pixelsf[4 * q + 1], t.pixelsf[4 * q + 2], t.pixelsf[4 * q + 3]));
+        } else {
+            if (!t.pixelsb && n) return bail(jt::fail(JT_ERR_INVALID, "texture without pixels"));
+            d.offset = (long long)texb.size();
+            for (size_t q = 0; q < n; q++)
+                texb.push_back(make_uchar4(t.pixelsb[4 * q], t.pixelsb[4 * q + 1], t.pixelsb[4 * q + 2], t.pixelsb[4 * q + 3]));
+        }
+    }
+    std::vector<DEnv> envs(scene->nenvironments);
+    for (int k = 0; k < scene->nenvironments; k++) {
+        const jt_environment& en = scene->environments[k];
+        DEnv& d = envs[k];
+        std::memset(&d, 0, sizeof(d));
+        jt::frame3 f = jt::load_frame(en.frame);
+        jt::store_frame(f, d.frame);
+        jt::store_frame(jt::inverse_frame(f, false), d.inv);
+        for (int q = 0; q < 3; q++) d.emission[q] = en.emission[q];
+        d.tex = en.emission_tex;
+    }
+    std::vector<DLight> dl(lights->nlights);
+    std::vector<float> cdf;
+    for (int k = 0; k < lights->nlights; k++) {
+        const jt_light& l = lights->lights[k];
+        dl[k] = DLight{l.instance, l.environment, (int)cdf.size(), l.ncdf};
+        cdf.insert(cdf.end(), l.cdf, l.cdf + l.ncdf);
+    }
+    std::vector<float> srgb, bytes;
+    build_luts(srgb, bytes);
+
+    DScene& S = c->S;
+    if ((st = upload(c, tlas, &S.tlas_nodes)) || (st = upload(c, tlas_prims, &S.tlas_prims)) ||
+        (st = upload(c, blas, &S.blas_nodes)) || (st = upload(c, prims, &S.prims)) ||
+        (st = upload(c, itrav, &S.inst_trav)) || (st = upload(c, ishade, &S.inst_shade)) ||
+        (st = upload(c, shapes, &S.shapes)) || (st = upload(c, pos, &S.pos)) || (st = upload(c, nrm, &S.nrm)) ||
+        (st = upload(c, tc, &S.tc)) || (st = upload(c, col, &S.col)) || (st = upload(c, elems, &S.elems)) ||
+        (st = upload(c, mats, &S.materials)) || (st = upload(c, texs, &S.textures)) || (st = upload(c, texb, &S.texb)) ||
+        (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) ||
+        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
+        return bail(st);
+    S.tlas_nnodes = bvh->tlas.nnodes;
+    S.nenvs = scene->nenvironments;
+    S.nlights = lights->nlights;
+
+    DParams& P = c->P;
+    const jt_camera& cam = scene->cameras[params->camera];
+    std::memcpy(P.cam.frame, cam.frame, sizeof(P.cam.frame));
+    P.cam.orthographic = cam.orthographic;
+    P.cam.lens = cam.lens;
+    P.cam.film = cam.film;
+    P.cam.aspect = (params->width > 0 && params->height > 0) ? (float)W / (float)H : cam.aspect;
+    P.cam.focus = cam.focus;
+    P.cam.aperture = cam.aperture;
+    P.width = W;
+    P.height = H;
+    P.bounces = params->bounces;
+    P.sampler = params->sampler;
+    P.clamp = (float)params->clamp;
+    P.envhidden = params->envhidden;
+    P.tentfilter = params->tentfilter;
+    P.nocaustics = params->nocaustics;
+    P.first = 0;
+    P.seed = params->seed;
+
+    // accumulators (make_trace_state: zeroed) + counters
+    const size_t np = (size_t)W * (size_t)H;
+    void *img, *alb, *nrmb, *hits, *cnt;
+    if ((e = hipMalloc(&img, np * 16)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc accumulators"));
+    c->allocations.push_back(img);
+    if ((e = hipMalloc(&alb, np * 16)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc accumulators"));
+    c->allocations.push_back(alb);
+    if ((e = hipMalloc(&nrmb, np * 16)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc accumulators"));
+    c->allocations.push_back(nrmb);
+    if ((e = hipMalloc(&hits, np * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc accumulators"));
+    c->allocations.push_back(hits);
+    if ((e = hipMalloc(&cnt, 8 * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc counters"));
+    c->allocations.push_back(cnt);
+    c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt};
+    st = jt_reset(c);
+    if (st != JT_OK) return bail(st);
+    *out = c;
+    return JT_OK;
+}
+
+int jt_reset(jt_ctx* c) {
+    if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    (void)hipSetDevice(c->device);
+    const size_t np = (size_t)c->width * (size_t)c->height;
+    hipError_t e;
+    if ((e = hipMemsetAsync(c->A.image, 0, np * 16, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->A.albedo, 0, np * 16, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->A.normal, 0, np * 16, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->A.hits, 0, np * 8, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->A.counters, 0, 64, c->stream)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync");
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    c->first = -1;
+    c->next = 0;
+    c->launches = 0;
+    c->kernel_ms = 0;
+    return JT_OK;
+}
+
+int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
+    if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    if (s0 < 0 || s1 < s0) return jt::fail(JT_ERR_STATE, "invalid sample range");
+    if (s0 == s1) return JT_OK;
+    if (c->first >= 0 && s0 != c->next)
+        return jt::fail(JT_ERR_STATE, "samples must be accumulated in order (expected " + std::to_string(c->next) + ")");
+    if (c->first < 0) c->first = s0;
+    c->P.first = c->first;
+    (void)hipSetDevice(c->device);
+    hipError_t e = hipEventRecord(c->ev0, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    e = c->sampler == JT_SAMPLER_NAIVE ? launch_s<2>(c->stack, c->S, c->P, s0, s1, c->A, c->stream)
+                                       : launch_s<1>(c->stack, c->S, c->P, s0, s1, c->A, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
+    if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    if ((e = hipEventSynchronize(c->ev1)) != hipSuccess) return hip_fail(e, "trace kernel");
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    c->kernel_ms += ms;
+    c->launches++;
+    c->next = s1;
+    return JT_OK;
+}
+
+int jt_trace_samples(jt_ctx* c) {
+    if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    const int n = c->first < 0 ? 0 : c->next;
+    if (n >= c->total_samples) return JT_OK;  // state.samples >= params.samples
+    const int target = std::min(n + c->batch, c->total_samples);
+    return jt_trace_range(c, n, target);
+}
+
+int jt_get_samples(const jt_ctx* c, int32_t* samples) {
+    if (!c || !samples) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    *samples = c->first < 0 ? 0 : c->next - c->first;
+    return JT_OK;
+}
+
+int jt_get_size(const jt_ctx* c, int32_t* w, int32_t* h) {
+    if (!c || !w || !h) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    *w = c->width;
+    *h = c->height;
+    return JT_OK;
+}
+
+int jt_get_image(jt_ctx* c, float* rgba) {
+    if (!c || !rgba) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    (void)hipSetDevice(c->device);
+    hipError_t e = hipMemcpy(rgba, c->A.image, (size_t)c->width * c->height * 16, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy image");
+}
+
+int jt_get_aovs(jt_ctx* c, float* albedo, float* normal, int64_t* hits) {
+    if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    (void)hipSetDevice(c->device);
+    const size_t np = (size_t)c->width * c->height;
+    std::vector<float4> tmp(np);
+    hipError_t e;
+    if (albedo) {
+        if ((e = hipMemcpy(tmp.data(), c->A.albedo, np * 16, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+        for (size_t k = 0; k < np; k++) {
+            albedo[3 * k] = tmp[k].x;
+            albedo[3 * k + 1] = tmp[k].y;
+            albedo[3 * k + 2] = tmp[k].z;
+        }
+    }
+    if (normal) {
+        if ((e = hipMemcpy(tmp.data(), c->A.normal, np * 16, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+        for (size_t k = 0; k < np; k++) {
+            normal[3 * k] = tmp[k].x;
+            normal[3 * k + 1] = tmp[k].y;
+            normal[3 * k + 2] = tmp[k].z;
+        }
+    }
+    if (hits) {
+        if ((e = hipMemcpy(hits, c->A.hits, np * 8, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+    }
+    return JT_OK;
+}
+
+int jt_get_counters(jt_ctx* c, jt_counters* out) {
+    if (!c || !out) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    (void)hipSetDevice(c->device);
+    unsigned long long v[8] = {0};
+    hipError_t e = hipMemcpy(v, c->A.counters, 7 * 8, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy counters");
+    out->paths = v[0];
+    out->rays = v[1];
+    out->light_queries = v[2];
+    out->nodes = v[3];
+    out->instances = v[4];
+    out->prims = v[5];
+    out->shades = v[6];
+    out->launches = c->launches;
+    out->kernel_ms = c->kernel_ms;
+    return JT_OK;
+}
+
+int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
+    if (!c || !out) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    out->image = c->A.image;
+    out->albedo = c->A.albedo;
+    out->normal = c->A.normal;
+    out->hits = c->A.hits;
+    out->width = c->width;
+    out->height = c->height;
+    out->stream = c->stream;
+    return JT_OK;
+}
+
+int jt_synchronize(jt_ctx* c) {
+    if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    (void)hipSetDevice(c->device);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    return e == hipSuccess ? JT_OK : hip_fail(e, "hipStreamSynchronize");
+}
+
+}  // extern "C"

@@ -1,0 +1,64 @@
+/*
+ * jt_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference hot path (Princic-1837592/julia-raytracer, src/trace.jl,
+ * src/bvh.jl, src/scene.jl, src/shading.jl, src/sampling.jl, src/geometry.jl, src/math.jl,
+ * src/color.jl). Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load it, and only as the checker / the timed CPU baseline — never as the product path.
+ *
+ * Parity status: the reference cannot run here (no Julia), ships no
+ * tests or golden vectors, and draws from an unseeded thread-local Xoshiro RNG. The oracle is
+ * pinned statistically against the reference's own render images/cornellbox_path.png
+ * (tests/golden/) and structurally against BVH shapes derived from src/bvh.jl.
+ */
+#ifndef JT_ORACLE_H
+#define JT_ORACLE_H
+
+#include "../include/jtrace.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_counters {
+    uint64_t paths, rays, light_queries, nodes, instances, prims, shades;
+} or_counters;
+
+/* make_scene_bvh (src/bvh.jl:66-88), independent of the product's host builder. */
+int or_build_scene_bvh(const jt_scene* scene, int32_t high_quality, jt_scene_bvh* out);
+void or_free_scene_bvh(jt_scene_bvh* bvh);
+
+/* make_trace_lights (src/trace.jl:117-187). */
+int or_make_lights(const jt_scene* scene, jt_lights* out);
+void or_free_lights(jt_lights* lights);
+
+/* trace_samples (src/trace.jl:215-274) over global samples [s0, s1) for all W*H pixels,
+ * running-mean weight 1/(s - first + 1). image: W*H*4, albedo/normal: W*H*3, hits: W*H.
+ * Rows are split over nthreads pthreads. Returns 0 or a negative jt_status. */
+int or_trace(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
+             const jt_params* params, int32_t width, int32_t height, int32_t first,
+             int32_t s0, int32_t s1, float* image, float* albedo, float* normal,
+             int64_t* hits, int32_t nthreads, or_counters* counters);
+
+/* Row-restricted variant: pixels of rows [row0, row1) only (bounded CPU samples). */
+int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
+                  const jt_params* params, int32_t width, int32_t height, int32_t row0,
+                  int32_t row1, int32_t first, int32_t s0, int32_t s1, float* image,
+                  float* albedo, float* normal, int64_t* hits, int32_t nthreads,
+                  or_counters* counters);
+
+/* Single-function known-answer entry points (tests/test_oracle_kat.py). */
+int or_intersect_triangle(const float* o, const float* d, float tmin, float tmax,
+                          const float* p1, const float* p2, const float* p3, float* out_uvt);
+int or_intersect_bbox(const float* o, const float* d, float tmin, float tmax,
+                      const float* bmin, const float* bmax);
+float or_fresnel_dielectric(float eta, const float* normal, const float* outgoing);
+void or_rng_first(uint64_t seed, int32_t pixel, int32_t sample, int32_t n, float* out);
+void or_inverse_frame(const float* frame, int32_t non_rigid, float* out);
+void or_srgb_to_rgb(const uint8_t* bytes, int32_t n, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,116 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU oracle (oracle/jt_oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+and only as the checker / the timed CPU baseline — never on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "build" / "libjt_oracle.so"
+
+
+def build():
+    subprocess.run(["make", "-C", str(HERE)], check=True, capture_output=True)
+
+
+def _load(abi):
+    if not LIB.exists():
+        build()
+    lib = C.CDLL(str(LIB))
+    lib.or_build_scene_bvh.argtypes = [C.POINTER(abi.jt_scene), C.c_int32, C.POINTER(abi.jt_scene_bvh)]
+    lib.or_free_scene_bvh.argtypes = [C.POINTER(abi.jt_scene_bvh)]
+    lib.or_free_scene_bvh.restype = None
+    lib.or_make_lights.argtypes = [C.POINTER(abi.jt_scene), C.POINTER(abi.jt_lights)]
+    lib.or_free_lights.argtypes = [C.POINTER(abi.jt_lights)]
+    lib.or_free_lights.restype = None
+    f32p, i64p = C.POINTER(C.c_float), C.POINTER(C.c_int64)
+    lib.or_trace_rows.argtypes = [C.POINTER(abi.jt_scene), C.POINTER(abi.jt_scene_bvh), C.POINTER(abi.jt_lights),
+                                  C.POINTER(abi.jt_params), C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                  C.c_int32, C.c_int32, C.c_int32, f32p, f32p, f32p, i64p, C.c_int32,
+                                  C.POINTER(Counters)]
+    lib.or_intersect_triangle.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p, f32p, f32p]
+    lib.or_intersect_bbox.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p]
+    lib.or_fresnel_dielectric.argtypes = [C.c_float, f32p, f32p]
+    lib.or_fresnel_dielectric.restype = C.c_float
+    lib.or_rng_first.argtypes = [C.c_uint64, C.c_int32, C.c_int32, C.c_int32, f32p]
+    lib.or_rng_first.restype = None
+    lib.or_inverse_frame.argtypes = [f32p, C.c_int32, f32p]
+    lib.or_inverse_frame.restype = None
+    lib.or_srgb_to_rgb.argtypes = [C.POINTER(C.c_uint8), C.c_int32, f32p]
+    lib.or_srgb_to_rgb.restype = None
+    return lib
+
+
+class Counters(C.Structure):
+    _fields_ = [("paths", C.c_uint64), ("rays", C.c_uint64), ("light_queries", C.c_uint64),
+                ("nodes", C.c_uint64), ("instances", C.c_uint64), ("prims", C.c_uint64),
+                ("shades", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class Oracle:
+    def __init__(self, abi):
+        self.abi = abi
+        self.lib = _load(abi)
+
+    def build_bvh(self, scene_abi, high_quality=False):
+        out = self.abi.jt_scene_bvh()
+        st = self.lib.or_build_scene_bvh(scene_abi.ref, int(high_quality), C.byref(out))
+        if st != 0:
+            raise RuntimeError(f"oracle bvh build failed: {st}")
+        return _Owned(out, self.lib.or_free_scene_bvh)
+
+    def make_lights(self, scene_abi):
+        out = self.abi.jt_lights()
+        st = self.lib.or_make_lights(scene_abi.ref, C.byref(out))
+        if st != 0:
+            raise RuntimeError(f"oracle lights failed: {st}")
+        return _Owned(out, self.lib.or_free_lights)
+
+    def trace(self, scene_abi, bvh, lights, params, width, height, s0, s1, first=0, rows=None,
+              nthreads=None, state=None):
+        """Returns (image (H,W,4), albedo (H,W,3), normal (H,W,3), hits (H,W), counters)."""
+        if nthreads is None:
+            nthreads = min(16, os.cpu_count() or 1)
+        if state is None:
+            image = np.zeros((height, width, 4), np.float32)
+            albedo = np.zeros((height, width, 3), np.float32)
+            normal = np.zeros((height, width, 3), np.float32)
+            hits = np.zeros((height, width), np.int64)
+        else:
+            image, albedo, normal, hits = state
+        r0, r1 = rows if rows is not None else (0, height)
+        cnt = Counters()
+        f32p = C.POINTER(C.c_float)
+        st = self.lib.or_trace_rows(scene_abi.ref, C.byref(bvh.struct), C.byref(lights.struct), C.byref(params),
+                                    width, height, r0, r1, first, s0, s1, image.ctypes.data_as(f32p),
+                                    albedo.ctypes.data_as(f32p), normal.ctypes.data_as(f32p),
+                                    hits.ctypes.data_as(C.POINTER(C.c_int64)), nthreads, C.byref(cnt))
+        if st != 0:
+            raise RuntimeError(f"oracle trace failed: {st}")
+        return image, albedo, normal, hits, cnt.as_dict()
+
+
+class _Owned:
+    def __init__(self, struct, free):
+        self.struct = struct
+        self._free = free
+
+    @property
+    def ref(self):
+        return C.byref(self.struct)
+
+    def __del__(self):
+        try:
+            self._free(C.byref(self.struct))
+        except Exception:
+            pass
