@@ -81,7 +81,7 @@ def main():
     ap.add_argument("--scene", default=str(ROOT / "assets" / "scenes" / "cornellbox" / "cornellbox.json"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-spp", type=int, default=2)
+    ap.add_argument("--cpu-spp", type=int, default=32)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -132,15 +132,23 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # counting pass: the same step with every traversal counter on (level 1); the timed steps
+    # run the production kernel (level 0: paths/rays/light queries). The counts are a
+    # deterministic function of (seed, samples, BVH); the ray count cross-checks them.
+    state.set_counters(1)
+    full = step()
+    state.set_counters(0)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     rays = 0
     kernel_ms = 0.0
-    agg = {k: 0 for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades", "launches")}
+    agg = {k: 0 for k in ("paths", "rays", "light_queries", "launches")}
     for _ in range(args.steps):
         c = step()
+        if c["rays"] != full["rays"] or c["light_queries"] != full["light_queries"]:
+            raise SystemExit(f"non-deterministic ray count: {c} vs counting pass {full}")
         for k in agg:
             agg[k] += c[k]
         kernel_ms += c["kernel_ms"]
@@ -163,13 +171,13 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         launches = max(1, agg["launches"])
         avg_launch_s = kernel_ms / launches / 1e3
-        per_launch = {k: v / launches for k, v in agg.items()}
+        per_launch = {k: v / max(1, full["launches"]) for k, v in full.items()}  # one step's launches
         bytes_per_launch = algorithmic_bytes(per_launch, shade_record_bytes(scene),
                                              any(len(s.quads) for s in scene.shapes))
         achieved = bytes_per_launch / avg_launch_s / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "trace_kernel<1,16>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "kernel": "trace_kernel<1,16,0>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                 "bytes_per_launch": int(bytes_per_launch),
                 "bytes_per_ray": round(bytes_per_launch / max(1.0, per_launch["rays"]), 1)}
         cpu = None
@@ -179,7 +187,7 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic-free: the reference's own cornellbox scene (assets/scenes), seeded RNG",
+            "data": "scene: the reference's own cornellbox (assets/scenes/cornellbox), seed 0x5EED",
             "config": {"workload": f"cornellbox path {W}x{H}x{S}spp", "scene": "cornellbox",
                        "sampler": args.sampler, "width": W, "height": H, "spp": S, "bounces": 8,
                        "parallelism": f"sample-range shards x{world} + RCCL reduce"},

@@ -270,6 +270,10 @@ int jt_get_aovs(jt_ctx* ctx, float* albedo, float* normal, int64_t* hits); /* W*
 int jt_get_counters(jt_ctx* ctx, jt_counters* out);
 int jt_reset(jt_ctx* ctx);                                           /* zero accumulators, samples = 0 */
 int jt_get_device_buffers(jt_ctx* ctx, jt_device_buffers* out);
+/* Counter level of subsequent launches: 1 (default) counts every jt_counters field; 0 counts
+ * paths, rays and light_queries only (the timed production kernel; the other fields are
+ * deterministic given seed + BVH and are taken from a level-1 launch of the same range). */
+int jt_set_counters(jt_ctx* ctx, int32_t level);
 int jt_synchronize(jt_ctx* ctx);
 void jt_destroy(jt_ctx* ctx);
 

@@ -162,19 +162,101 @@ __device__ __forceinline__ int jl_clampi(int x, int lo, int hi) { return x > hi 
 __device__ __forceinline__ float max3(v3 a) { return jl_max(jl_max(a.x, a.y), a.z); }
 
 #if JT_EXACT_MATH
-__device__ __forceinline__ float jl_sin(float x) { return (float)sin((double)x); }
-__device__ __forceinline__ float jl_cos(float x) { return (float)cos((double)x); }
+// Double-evaluated, once-rounded transcendentals (the float contract). The hot-path arguments
+// of sin/cos (2*pi*u, atan(...), v*pi, u*2*pi) lie in [0, 2*pi]; for |x| < 2^19 a Cody-Waite
+// reduction by pi/2 with a 33-bit leading constant is exact in double and the fdlibm kernels
+// give < 1 ulp in double, so rounding to float reproduces the correctly rounded float except
+// within ~2^-52 of a rounding midpoint. Larger arguments fall back to ocml's double sincos.
+__device__ __forceinline__ void dsincos_small(double x, double& s, double& c) {
+    const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+                 pio2_1t = 6.07710050650619224932e-11;
+    const double n = __builtin_rint(x * invpio2);
+    const double r = (x - n * pio2_1) - n * pio2_1t;
+    const double z = r * r;
+    // __kernel_sin / __kernel_cos (fdlibm k_sin.c / k_cos.c), tail y = 0
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double sr = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    const double ks = r + (z * r) * (S1 + z * sr);
+    const double cr = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double kc = w + (((1.0 - w) - hz) + z * cr);
+    const int q = (int)n & 3;
+    s = q == 0 ? ks : (q == 1 ? kc : (q == 2 ? -ks : -kc));
+    c = q == 0 ? kc : (q == 1 ? -ks : (q == 2 ? -kc : ks));
+}
+__device__ __noinline__ void dsincos_large(double x, double* s, double* c) { sincos(x, s, c); }
 __device__ __forceinline__ void jl_sincos(float x, float* s, float* c) {
     double sd, cd;
-    sincos((double)x, &sd, &cd);
+    if (__builtin_fabsf(x) < 524288.0f) {
+        dsincos_small((double)x, sd, cd);
+    } else {
+        dsincos_large((double)x, &sd, &cd);
+    }
     *s = (float)sd;
     *c = (float)cd;
 }
-__device__ __forceinline__ float jl_atan(float x) { return (float)atan((double)x); }
-__device__ __forceinline__ float jl_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
-__device__ __forceinline__ float jl_acos(float x) { return (float)acos((double)x); }
-__device__ __forceinline__ float jl_log(float x) { return (float)log((double)x); }
-__device__ __forceinline__ float jl_exp(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float jl_sin(float x) {
+    float s, c;
+    jl_sincos(x, &s, &c);
+    return s;
+}
+__device__ __forceinline__ float jl_cos(float x) {
+    float s, c;
+    jl_sincos(x, &s, &c);
+    return c;
+}
+// atan in double (fdlibm s_atan.c), used by sample_microfacet on every rough specular sample
+__device__ __forceinline__ float jl_atan(float xf) {
+    const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
+                              1.57079632679489655800e+00};
+    const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
+                              6.12323399573676603587e-17};
+    const double a0 = 3.33333333333329318027e-01, a1 = -1.99999999998764832476e-01, a2 = 1.42857142725034663711e-01,
+                 a3 = -1.11111104054623557880e-01, a4 = 9.09088713343650656196e-02, a5 = -7.69187620504482999495e-02,
+                 a6 = 6.66107313738753120669e-02, a7 = -5.83357013379057348645e-02, a8 = 4.97687799461593236017e-02,
+                 a9 = -3.65315727442169155270e-02, a10 = 1.62858201153657823623e-02;
+    if (__builtin_isnan(xf)) return xf;
+    const double x0 = (double)xf;
+    double x = __builtin_fabs(x0);
+    int id;
+    if (x < 0.4375) {
+        if (x < 1.0e-29) return xf;
+        id = -1;
+    } else if (x < 1.1875) {
+        if (x < 0.6875) {
+            id = 0;
+            x = (2.0 * x - 1.0) / (2.0 + x);
+        } else {
+            id = 1;
+            x = (x - 1.0) / (x + 1.0);
+        }
+    } else if (x < 2.4375) {
+        id = 2;
+        x = (x - 1.5) / (1.0 + 1.5 * x);
+    } else if (x < 1.0e17) {
+        id = 3;
+        x = -1.0 / x;
+    } else {
+        return (float)__builtin_copysign(atanhi[3] + atanlo[3], x0);
+    }
+    const double z = x * x, w = z * z;
+    const double s1 = z * (a0 + w * (a2 + w * (a4 + w * (a6 + w * (a8 + w * a10)))));
+    const double s2 = w * (a1 + w * (a3 + w * (a5 + w * (a7 + w * a9))));
+    double r;
+    if (id < 0) r = x - x * (s1 + s2);
+    else r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return (float)__builtin_copysign(r, x0);
+}
+// rare-path transcendentals (environment, volumes): ocml double, kept out of line
+__device__ __noinline__ float jl_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+__device__ __noinline__ float jl_acos(float x) { return (float)acos((double)x); }
+__device__ __noinline__ float jl_log(float x) { return (float)log((double)x); }
+__device__ __noinline__ float jl_exp(float x) { return (float)exp((double)x); }
 #else
 __device__ __forceinline__ float jl_sin(float x) { return sinf(x); }
 __device__ __forceinline__ float jl_cos(float x) { return cosf(x); }

@@ -247,6 +247,7 @@ struct Counters {
 // One traversal loop for intersect_scene_bvh (root = TLAS node 0) and intersect_instance_bvh
 // (root = one instance entry). Closest hit; a primitive with t == tmax replaces the current hit,
 // exactly as the reference's `t > ray.tmax -> reject` test in the reference's visit order.
+template <int COUNT>
 __device__ __forceinline__ Hit traverse(const DScene& S, v3 wo, v3 wd, unsigned root, int* stack, Counters& cnt) {
     Hit h{-1, -1, 0, 0, 0, false};
     float tmax = __builtin_inff();
@@ -264,7 +265,7 @@ __device__ __forceinline__ Hit traverse(const DScene& S, v3 wo, v3 wd, unsigned 
         if (type == T_INST) {
             // instance visit: inverse(frame, true) precomputed on the host (src/bvh.jl:345,502)
             const DInstTrav it = S.inst_trav[idx];
-            cnt.instances++;
+            if (COUNT) cnt.instances++;
             const fr3 inv = frame_from(it.i0, it.i1, it.i2);
             lo = transform_point(inv, wo);
             ld = transform_vector(inv, wd);
@@ -277,7 +278,7 @@ __device__ __forceinline__ Hit traverse(const DScene& S, v3 wo, v3 wd, unsigned 
         }
         const bool blas = type == T_BLAS;
         const DNode nd = blas ? S.blas_nodes[idx] : S.tlas_nodes[idx];
-        cnt.nodes++;
+        if (COUNT) cnt.nodes++;
         const v3 o = blas ? lo : wo;
         const v3 dv = blas ? ldinv : wdinv;
         if (!intersect_bbox(o, dv, tmin, tmax, nd.a, nd.b)) continue;
@@ -303,7 +304,7 @@ __device__ __forceinline__ Hit traverse(const DScene& S, v3 wo, v3 wd, unsigned 
             for (int k = 0; k < num; k++) {
                 const float4* r = S.prims + 3 * (start + k);
                 const float4 a = r[0], b = r[1], c = r[2];
-                cnt.prims++;
+                if (COUNT) cnt.prims++;
                 PrimHit p = intersect_triangle(lo, ld, tmin, tmax, xyz(a), xyz(b), xyz(c));
                 if (p.hit) {
                     h = Hit{cur_inst, __float_as_int(a.w), p.u, p.v, p.t, true};
@@ -314,7 +315,7 @@ __device__ __forceinline__ Hit traverse(const DScene& S, v3 wo, v3 wd, unsigned 
             for (int k = 0; k < num; k++) {
                 const float4* r = S.prims + 4 * (start + k);
                 const float4 a = r[0], b = r[1], c = r[2], d = r[3];
-                cnt.prims++;
+                if (COUNT) cnt.prims++;
                 PrimHit p = intersect_quad(lo, ld, tmin, tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
                 if (p.hit) {
                     h = Hit{cur_inst, __float_as_int(a.w), p.u, p.v, p.t, true};
@@ -352,57 +353,261 @@ __device__ __forceinline__ v3 sample_lights(const DScene& S, v3 position, float 
     }
     return V3(0, 0, 0);
 }
-// sample_lights_pdf (src/trace.jl:1010-1084)
-__device__ __forceinline__ float sample_lights_pdf(const DScene& S, v3 position, v3 direction, int* stack, Counters& cnt) {
-    float pdf = 0.0f;
-    for (int li = 0; li < S.nlights; li++) {
-        const DLight l = S.lights[li];
-        const float* cdf = S.cdf + l.cdf_offset;
-        if (l.instance >= 0) {
-            float lpdf = 0.0f;
-            v3 next_position = position;
-            const float area = cdf[l.ncdf - 1];
-            for (int bounce = 0; bounce < 100; bounce++) {
-                cnt.light_queries++;
-                Hit h = traverse(S, next_position, direction, (T_INST << 30) | (unsigned)l.instance, stack, cnt);
-                if (!h.hit) break;
-                v3 lposition = eval_position(S, l.instance, h.elem, V2(h.u, h.v));
-                v3 lnormal = eval_element_normal(S, l.instance, h.elem);
-                v3 dd = lposition - position;
-                lpdf += dot(dd, dd) / (__builtin_fabsf(dot(lnormal, direction)) * area);
-                next_position = lposition + direction * 0.001f;
-            }
-            pdf += lpdf;
-        } else if (l.environment >= 0) {
-            const DEnv& env = S.envs[l.environment];
-            const DTexture t = S.textures[env.tex];
-            v3 wl = transform_direction(frame_from(env.inv), direction);
-            v2 tc = V2(jl_atan2(wl.z, wl.x) / (2 * pif), jl_acos(jl_clamp(wl.y, -1.0f, 1.0f)) / pif);
-            if (tc.x < 0) tc.x = tc.x + 1;
-            int i = jl_clampi((int)__builtin_truncf(tc.x * (float)t.width), 0, t.width - 1);
-            int j = jl_clampi((int)__builtin_truncf(tc.y * (float)t.height), 0, t.height - 1);
-            float prob = sample_discrete_pdf(cdf, j * t.width + i + 1) / cdf[l.ncdf - 1];
-            float angle = (2 * pif / (float)t.width) * (pif / (float)t.height) *
-                          jl_sin(pif * ((float)j + 0.5f) / (float)t.height);
-            pdf += prob / angle;
-        }
-    }
-    pdf *= sample_uniform_pdf(S.nlights);
-    return pdf;
+// env-light term of sample_lights_pdf (src/trace.jl:1045-1079)
+__device__ __noinline__ float env_light_pdf(const DScene& S, const DLight l, v3 direction) {
+    const float* cdf = S.cdf + l.cdf_offset;
+    const DEnv& env = S.envs[l.environment];
+    const DTexture t = S.textures[env.tex];
+    v3 wl = transform_direction(frame_from(env.inv), direction);
+    v2 tc = V2(jl_atan2(wl.z, wl.x) / (2 * pif), jl_acos(jl_clamp(wl.y, -1.0f, 1.0f)) / pif);
+    if (tc.x < 0) tc.x = tc.x + 1;
+    int i = jl_clampi((int)__builtin_truncf(tc.x * (float)t.width), 0, t.width - 1);
+    int j = jl_clampi((int)__builtin_truncf(tc.y * (float)t.height), 0, t.height - 1);
+    float prob = sample_discrete_pdf(cdf, j * t.width + i + 1) / cdf[l.ncdf - 1];
+    float angle = (2 * pif / (float)t.width) * (pif / (float)t.height) *
+                  jl_sin(pif * ((float)j + 0.5f) / (float)t.height);
+    return prob / angle;
 }
 
 // ============================================================================ integrator
+// trace_path / trace_naive restated as a per-lane state machine. Every iteration of the
+// kernel's loop issues exactly one BVH query per lane — a closest-hit scene query (PH_SCENE)
+// or one intersect_instance_bvh query of sample_lights_pdf (PH_LIGHT) — through the single
+// `traverse` call site, then advances the lane's state. Float operations and RNG draws happen
+// in exactly the reference's order; only where the lane waits between them changes.
+enum : int { PH_SCENE = 0, PH_LIGHT = 1 };
+enum : int { F_HIT = 1, F_VOLUME = 2 };
+
 struct Path {
-    v3 o, d;      // current ray (tmin = ray_eps, tmax = inf at each query)
-    v3 cam_d;     // camera ray direction (the normal AOV's fallback, src/trace.jl:642,647)
-    v3 radiance, weight;
-    v3 hit_albedo, hit_normal;
-    Volume vol;
-    float max_roughness;
-    int bounce, opbounce, cur_volume;
-    bool hit;
+    v3 o, d;                    // pending ray; during PH_LIGHT: shading position / incoming
+    v3 radiance, weight;  // during PH_LIGHT weight already holds weight .* f (src/trace.jl:386)
     Rng rng;
+    int bounce, opbounce, flags, phase;
+    float max_roughness;
+    // sample_lights_pdf in flight (src/trace.jl:1010-1084)
+    int li, lcount;
+    v3 lq;       // next_position of the current instance light
+    float pb;    // sample_bsdfcos_pdf / sample_scattering_pdf
+    float pdf, lpdf;
+    Volume vol;  // volume_stack[1] (the stack never holds more than one entry)
 };
+
+// while bounce < params.bounces: bounce += 1 (src/trace.jl:295-297, 487-489)
+__device__ __forceinline__ bool next_bounce(const DParams& P, Path& st) {
+    if (st.bounce >= P.bounces) return true;
+    st.bounce += 1;
+    st.phase = PH_SCENE;
+    return false;
+}
+// end of a bounce: weight checks and Russian roulette (src/trace.jl:455-465, 557-567)
+__device__ __forceinline__ bool after_weight(const DParams& P, Path& st) {
+    if (is_zero(st.weight) || !all_finite(st.weight)) return true;
+    if (st.bounce > 3) {
+        float rr_prob = jl_min(0.99f, max3(st.weight));
+        if (rand1f(st.rng) >= rr_prob) return true;
+        st.weight = st.weight * (1 / rr_prob);
+    }
+    return next_bounce(P, st);
+}
+// walk the light list: environment terms are added in place, an instance light starts its
+// query chain; after the last light the one-sample MIS weight is applied (src/trace.jl:386-397)
+__device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P, Path& st) {
+    for (;;) {
+        st.li += 1;
+        if (st.li >= S.nlights) {
+            const float pdf = st.pdf * sample_uniform_pdf(S.nlights);
+            st.weight = st.weight / (0.5f * st.pb + 0.5f * pdf);  // (weight .* f) / (...)
+            return after_weight(P, st);
+        }
+        const DLight l = S.lights[st.li];
+        if (l.instance >= 0) {
+            st.lpdf = 0.0f;
+            st.lcount = 0;
+            st.lq = st.o;
+            st.phase = PH_LIGHT;
+            return false;
+        }
+        if (l.environment >= 0) st.pdf += env_light_pdf(S, l, st.d);
+    }
+}
+__device__ __forceinline__ bool begin_light_pdf(const DScene& S, const DParams& P, Path& st) {
+    st.pdf = 0.0f;
+    st.li = -1;
+    return light_advance(S, P, st);
+}
+// one intersect_instance_bvh result of the instance-light loop (src/trace.jl:1024-1044)
+__device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Path& st, const Hit& h) {
+    if (h.hit) {
+        const DLight l = S.lights[st.li];
+        v3 lposition = eval_position(S, l.instance, h.elem, V2(h.u, h.v));
+        v3 lnormal = eval_element_normal(S, l.instance, h.elem);
+        const float area = S.cdf[l.cdf_offset + l.ncdf - 1];
+        v3 dd = lposition - st.o;
+        st.lpdf += dot(dd, dd) / (__builtin_fabsf(dot(lnormal, st.d)) * area);
+        st.lq = lposition + st.d * 0.001f;
+        if (++st.lcount < 100) return false;
+    }
+    st.pdf += st.lpdf;
+    return light_advance(S, P, st);
+}
+
+// trace_path's bounce body after the closest-hit query (src/trace.jl:298-453)
+// The albedo/normal running means (src/trace.jl:635-636) are updated as soon as the bounce-0
+// surface is accepted — their targets are final at that point — so they are not path state.
+struct Aov {
+    float4* albedo;
+    float4* normal;
+    int pixel;
+    float w;
+};
+__device__ __forceinline__ void aov_update(const Aov& a, v3 ta, v3 tn) {
+    const float omw = 1 - a.w;
+    float4 alb = a.albedo[a.pixel], nrm = a.normal[a.pixel];
+    a.albedo[a.pixel] = make_float4(alb.x * omw + ta.x * a.w, alb.y * omw + ta.y * a.w, alb.z * omw + ta.z * a.w, 0.0f);
+    a.normal[a.pixel] = make_float4(nrm.x * omw + tn.x * a.w, nrm.y * omw + tn.y * a.w, nrm.z * omw + tn.z * a.w, 0.0f);
+}
+
+__device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const Aov& aov,
+                                         unsigned& shades) {
+    if (!isec.hit) {
+        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment(S, st.d);
+        return true;
+    }
+    bool in_volume = false;
+    if (st.flags & F_VOLUME) {  // :307-326
+        float rl = rand1f(st.rng), rd = rand1f(st.rng);
+        float distance = sample_transmittance(st.vol.density, isec.t, rl, rd);
+        v3 tr = eval_transmittance(st.vol.density, distance);
+        float tp = sample_transmittance_pdf(st.vol.density, distance, isec.t);
+        st.weight = (st.weight * tr) / tp;
+        in_volume = distance < isec.t;
+        isec.t = distance;
+    }
+    if (!in_volume) {  // surface (:328-423)
+        v3 outgoing = -st.d;
+        Shading sh;
+        eval_shading(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
+        shades++;
+        if (P.nocaustics) {
+            st.max_roughness = jl_max(sh.mat.roughness, st.max_roughness);
+            sh.mat.roughness = st.max_roughness;
+        }
+        if (sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
+            if (st.opbounce > 128) return true;
+            st.opbounce += 1;
+            st.o = sh.position + st.d * 0.01f;
+            st.bounce -= 1;
+            return next_bounce(P, st);
+        }
+        if (st.bounce == 0) {
+            st.flags |= F_HIT;
+            aov_update(aov, sh.mat.color, sh.normal);
+        }
+        st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
+        v3 incoming;
+        const bool delta = is_delta(sh.mat);
+        if (!delta) {
+            if (rand1f(st.rng) < 0.5f) {
+                float rnl = rand1f(st.rng);
+                v2 rn = rand2f(st.rng);
+                incoming = sample_bsdfcos(sh.mat, sh.normal, outgoing, rnl, rn);
+            } else {
+                float rl = rand1f(st.rng), rel = rand1f(st.rng);
+                v2 ruv = rand2f(st.rng);
+                incoming = sample_lights(S, sh.position, rl, rel, ruv);
+            }
+            if (is_zero(incoming)) return true;
+            st.weight = st.weight * eval_bsdfcos(sh.mat, sh.normal, outgoing, incoming);
+            st.pb = sample_bsdfcos_pdf(sh.mat, sh.normal, outgoing, incoming);
+        } else {
+            float rnl = rand1f(st.rng);
+            incoming = sample_delta(sh.mat, sh.normal, outgoing, rnl);
+            v3 f = eval_delta(sh.mat, sh.normal, outgoing, incoming);
+            float pd = sample_delta_pdf(sh.mat, sh.normal, outgoing, incoming);
+            st.weight = (st.weight * f) / pd;
+        }
+        // volume stack push/pop (:405-421); independent of the weight update it follows
+        const int mtype = sh.mat.type;
+        if ((mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE) &&
+            dot(sh.normal, outgoing) * dot(sh.normal, incoming) < 0) {
+            if (!(st.flags & F_VOLUME)) {
+                st.flags |= F_VOLUME;  // eval_material again: only the volume fields are kept
+                st.vol.density = sh.mat.density;
+                st.vol.scattering = sh.mat.scattering;
+                st.vol.scanisotropy = sh.mat.scanisotropy;
+            } else {
+                st.flags &= ~F_VOLUME;
+            }
+        }
+        st.o = sh.position;
+        st.d = incoming;
+        return delta ? after_weight(P, st) : begin_light_pdf(S, P, st);
+    }
+    // volume scattering (:424-453)
+    v3 outgoing = -st.d;
+    v3 position = st.o + st.d * isec.t;
+    v3 incoming;
+    if (rand1f(st.rng) < 0.5f) {
+        (void)rand1f(st.rng);  // rnl: drawn, unused by sample_scattering
+        v2 rn = rand2f(st.rng);
+        incoming = sample_scattering(st.vol, outgoing, rn);
+    } else {
+        float rl = rand1f(st.rng), rel = rand1f(st.rng);
+        v2 ruv = rand2f(st.rng);
+        incoming = sample_lights(S, position, rl, rel, ruv);
+    }
+    if (is_zero(incoming)) return true;
+    st.weight = st.weight * eval_scattering(st.vol, outgoing, incoming);
+    st.pb = sample_scattering_pdf(st.vol, outgoing, incoming);
+    st.o = position;
+    st.d = incoming;
+    return begin_light_pdf(S, P, st);
+}
+
+// trace_naive's bounce body after the closest-hit query (src/trace.jl:490-569)
+__device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const Aov& aov,
+                                          unsigned& shades) {
+    if (!isec.hit) {
+        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment(S, st.d);
+        return true;
+    }
+    v3 outgoing = -st.d;
+    Shading sh;
+    eval_shading(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
+    shades++;
+    if (sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
+        if (st.opbounce > 128) return true;
+        st.opbounce += 1;
+        st.o = sh.position + st.d * 0.01f;
+        st.bounce -= 1;
+        return next_bounce(P, st);
+    }
+    if (st.bounce == 0) {
+        st.flags |= F_HIT;
+        aov_update(aov, sh.mat.color, sh.normal);
+    }
+    st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
+    v3 incoming, f;
+    float p;
+    if (sh.mat.roughness != 0) {
+        float rnl = rand1f(st.rng);
+        v2 rn = rand2f(st.rng);
+        incoming = sample_bsdfcos(sh.mat, sh.normal, outgoing, rnl, rn);
+        if (is_zero(incoming)) return true;
+        f = eval_bsdfcos(sh.mat, sh.normal, outgoing, incoming);
+        p = sample_bsdfcos_pdf(sh.mat, sh.normal, outgoing, incoming);
+    } else {
+        float rnl = rand1f(st.rng);
+        incoming = sample_delta(sh.mat, sh.normal, outgoing, rnl);
+        if (is_zero(incoming)) return true;
+        f = eval_delta(sh.mat, sh.normal, outgoing, incoming);
+        p = sample_delta_pdf(sh.mat, sh.normal, outgoing, incoming);
+    }
+    st.weight = (st.weight * f) / p;
+    st.o = sh.position;
+    st.d = incoming;
+    return after_weight(P, st);
+}
 
 // eval_camera (src/scene.jl:372-411)
 __device__ __forceinline__ void eval_camera(const DCamera& cam, v2 image_uv, v2 lens_uv, v3& ro, v3& rd) {
@@ -442,182 +647,18 @@ __device__ __forceinline__ void start_path(const DParams& P, int i, int j, int p
         uv = V2(((float)i + fuv.x) / (float)P.width, ((float)j + fuv.y) / (float)P.height);
     }
     eval_camera(P.cam, uv, sample_disk(luv), st.o, st.d);
-    st.cam_d = st.d;
     st.radiance = V3(0, 0, 0);
     st.weight = V3(1, 1, 1);
-    st.hit_albedo = V3(0, 0, 0);
-    st.hit_normal = V3(0, 0, 0);
-    st.vol = Volume{V3(0, 0, 0), V3(0, 0, 0), 0.0f};
     st.max_roughness = 0.0f;
-    st.bounce = -1;
+    st.bounce = 0;  // the first loop iteration: bounce = -1 + 1 (bounces >= 0 always enters)
     st.opbounce = 0;
-    st.cur_volume = 0;
-    st.hit = false;
+    st.flags = 0;
+    st.phase = PH_SCENE;
 }
 
-// One iteration of trace_path's bounce loop (src/trace.jl:296-466). Returns true when the path
-// is finished (the reference's `break` or the loop condition failing).
-__device__ __forceinline__ bool step_path(const DScene& S, const DParams& P, Path& st, int* stack, Counters& cnt) {
-    if (st.bounce >= P.bounces) return true;
-    st.bounce += 1;
-    cnt.rays++;
-    Hit isec = traverse(S, st.o, st.d, T_TLAS << 30, stack, cnt);
-    if (!isec.hit) {
-        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment(S, st.d);
-        return true;
-    }
-    bool in_volume = false;
-    if (st.cur_volume != 0) {  // :307-326
-        float rl = rand1f(st.rng), rd = rand1f(st.rng);
-        float distance = sample_transmittance(st.vol.density, isec.t, rl, rd);
-        v3 tr = eval_transmittance(st.vol.density, distance);
-        float tp = sample_transmittance_pdf(st.vol.density, distance, isec.t);
-        st.weight = (st.weight * tr) / tp;
-        in_volume = distance < isec.t;
-        isec.t = distance;
-    }
-    v3 incoming;
-    if (!in_volume) {  // surface (:328-423)
-        v3 outgoing = -st.d;
-        Shading sh;
-        eval_shading(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
-        cnt.shades++;
-        if (P.nocaustics) {
-            st.max_roughness = jl_max(sh.mat.roughness, st.max_roughness);
-            sh.mat.roughness = st.max_roughness;
-        }
-        if (sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
-            if (st.opbounce > 128) return true;
-            st.opbounce += 1;
-            st.o = sh.position + st.d * 0.01f;
-            st.bounce -= 1;
-            return false;
-        }
-        if (st.bounce == 0) {
-            st.hit = true;
-            st.hit_albedo = sh.mat.color;
-            st.hit_normal = sh.normal;
-        }
-        st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
-        if (!is_delta(sh.mat)) {
-            if (rand1f(st.rng) < 0.5f) {
-                float rnl = rand1f(st.rng);
-                v2 rn = rand2f(st.rng);
-                incoming = sample_bsdfcos(sh.mat, sh.normal, outgoing, rnl, rn);
-            } else {
-                float rl = rand1f(st.rng), rel = rand1f(st.rng);
-                v2 ruv = rand2f(st.rng);
-                incoming = sample_lights(S, sh.position, rl, rel, ruv);
-            }
-            if (is_zero(incoming)) return true;
-            v3 f = eval_bsdfcos(sh.mat, sh.normal, outgoing, incoming);
-            float pb = sample_bsdfcos_pdf(sh.mat, sh.normal, outgoing, incoming);
-            float pl = sample_lights_pdf(S, sh.position, incoming, stack, cnt);
-            st.weight = (st.weight * f) / (0.5f * pb + 0.5f * pl);
-        } else {
-            float rnl = rand1f(st.rng);
-            incoming = sample_delta(sh.mat, sh.normal, outgoing, rnl);
-            v3 f = eval_delta(sh.mat, sh.normal, outgoing, incoming);
-            float pd = sample_delta_pdf(sh.mat, sh.normal, outgoing, incoming);
-            st.weight = (st.weight * f) / pd;
-        }
-        const int mtype = S.inst_shade[isec.inst].mat_type;  // is_volumetric(scene, instance)
-        if ((mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE) &&
-            dot(sh.normal, outgoing) * dot(sh.normal, incoming) < 0) {
-            if (st.cur_volume == 0) {
-                // eval_material again (without the nocaustics override): only the volume fields
-                st.cur_volume += 1;
-                st.vol.density = sh.mat.density;
-                st.vol.scattering = sh.mat.scattering;
-                st.vol.scanisotropy = sh.mat.scanisotropy;
-            } else {
-                st.cur_volume -= 1;
-            }
-        }
-        st.o = sh.position;
-        st.d = incoming;
-    } else {  // volume scattering (:424-453)
-        v3 outgoing = -st.d;
-        v3 position = st.o + st.d * isec.t;
-        if (rand1f(st.rng) < 0.5f) {
-            rand1f(st.rng);  // rnl: drawn, unused by sample_scattering
-            v2 rn = rand2f(st.rng);
-            incoming = sample_scattering(st.vol, outgoing, rn);
-        } else {
-            float rl = rand1f(st.rng), rel = rand1f(st.rng);
-            v2 ruv = rand2f(st.rng);
-            incoming = sample_lights(S, position, rl, rel, ruv);
-        }
-        if (is_zero(incoming)) return true;
-        v3 f = eval_scattering(st.vol, outgoing, incoming);
-        float ps = sample_scattering_pdf(st.vol, outgoing, incoming);
-        float pl = sample_lights_pdf(S, position, incoming, stack, cnt);
-        st.weight = (st.weight * f) / (0.5f * ps + 0.5f * pl);
-        st.o = position;
-        st.d = incoming;
-    }
-    if (is_zero(st.weight) || !all_finite(st.weight)) return true;
-    if (st.bounce > 3) {  // Russian roulette (:459-465)
-        float rr_prob = jl_min(0.99f, max3(st.weight));
-        if (rand1f(st.rng) >= rr_prob) return true;
-        st.weight = st.weight * (1 / rr_prob);
-    }
-    return false;
-}
-
-// One iteration of trace_naive's bounce loop (src/trace.jl:488-570).
-__device__ __forceinline__ bool step_naive(const DScene& S, const DParams& P, Path& st, int* stack, Counters& cnt) {
-    if (st.bounce >= P.bounces) return true;
-    st.bounce += 1;
-    cnt.rays++;
-    Hit isec = traverse(S, st.o, st.d, T_TLAS << 30, stack, cnt);
-    if (!isec.hit) {
-        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment(S, st.d);
-        return true;
-    }
-    v3 outgoing = -st.d;
-    Shading sh;
-    eval_shading(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
-    cnt.shades++;
-    if (sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
-        if (st.opbounce > 128) return true;
-        st.opbounce += 1;
-        st.o = sh.position + st.d * 0.01f;
-        st.bounce -= 1;
-        return false;
-    }
-    if (st.bounce == 0) {
-        st.hit = true;
-        st.hit_albedo = sh.mat.color;
-        st.hit_normal = sh.normal;
-    }
-    st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
-    v3 incoming;
-    if (sh.mat.roughness != 0) {
-        float rnl = rand1f(st.rng);
-        v2 rn = rand2f(st.rng);
-        incoming = sample_bsdfcos(sh.mat, sh.normal, outgoing, rnl, rn);
-        if (is_zero(incoming)) return true;
-        v3 f = eval_bsdfcos(sh.mat, sh.normal, outgoing, incoming);
-        float p = sample_bsdfcos_pdf(sh.mat, sh.normal, outgoing, incoming);
-        st.weight = (st.weight * f) / p;
-    } else {
-        float rnl = rand1f(st.rng);
-        incoming = sample_delta(sh.mat, sh.normal, outgoing, rnl);
-        if (is_zero(incoming)) return true;
-        v3 f = eval_delta(sh.mat, sh.normal, outgoing, incoming);
-        float p = sample_delta_pdf(sh.mat, sh.normal, outgoing, incoming);
-        st.weight = (st.weight * f) / p;
-    }
-    if (is_zero(st.weight) || !all_finite(st.weight)) return true;
-    if (st.bounce > 3) {
-        float rr_prob = jl_min(0.99f, max3(st.weight));
-        if (rand1f(st.rng) >= rr_prob) return true;
-        st.weight = st.weight * (1 / rr_prob);
-    }
-    st.o = sh.position;
-    st.d = incoming;
-    return false;
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
 }
 
 struct DAccum {
@@ -628,14 +669,10 @@ struct DAccum {
     unsigned long long* counters;  // 7 x u64: paths rays light_queries nodes instances prims shades
 };
 
-__device__ __forceinline__ unsigned wave_sum(unsigned v) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
-// 16x16-pixel workgroups; regenerates paths until the lane's samples are done.
-template <int SAMPLER, int STACK>
+// 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
+// mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
+template <int SAMPLER, int STACK, int COUNT>
 __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     __shared__ int lds_stack[STACK * BLOCK];
     int* stack = lds_stack + threadIdx.x;
@@ -645,13 +682,21 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     if (i < P.width && j < P.height && s_begin < s_end) {
         const int pixel = j * P.width + i;
-        float4 img = A.image[pixel], alb = A.albedo[pixel], nrm = A.normal[pixel];
-        long long hits = A.hits[pixel];
         int sample = s_begin;
+        Aov aov{A.albedo, A.normal, pixel, 1.0f / (float)(sample - P.first + 1)};
         Path st;
         start_path(P, i, j, pixel, sample, st);
         for (;;) {
-            const bool done = SAMPLER == 2 ? step_naive(S, P, st, stack, cnt) : step_path(S, P, st, stack, cnt);
+            const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
+            const v3 qo = light ? st.lq : st.o;
+            const unsigned root = light ? ((T_INST << 30) | (unsigned)S.lights[st.li].instance) : (T_TLAS << 30);
+            if (light) cnt.light_queries++;
+            else cnt.rays++;
+            const Hit h = traverse<COUNT>(S, qo, st.d, root, stack, cnt);
+            bool done;
+            if (light) done = light_hit(S, P, st, h);
+            else if (SAMPLER == 2) done = naive_hit(S, P, st, h, aov, cnt.shades);
+            else done = path_hit(S, P, st, h, aov, cnt.shades);
             if (!done) continue;
             // trace_sample epilogue (src/trace.jl:625-648)
             cnt.paths++;
@@ -659,39 +704,25 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
             if (!all_finite(radiance)) radiance = V3(0, 0, 0);
             const float mr = max3(radiance);
             if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
-            const float w = 1.0f / (float)(sample - P.first + 1);
+            const float w = aov.w;
             const float omw = 1 - w;
-            v4 target;
-            v3 ta, tn;
-            if (st.hit) {
-                target = V4(radiance.x, radiance.y, radiance.z, 1);
-                ta = st.hit_albedo;
-                tn = st.hit_normal;
-                hits += 1;
-            } else if (!P.envhidden && S.nenvs != 0) {
-                target = V4(radiance.x, radiance.y, radiance.z, 1);
-                ta = V3(1, 1, 1);
-                tn = -st.cam_d;
-                hits += 1;
-            } else {
-                target = V4(0, 0, 0, 0);
-                ta = V3(0, 0, 0);
-                tn = -st.cam_d;
-            }
-            img = make_float4(img.x * omw + target.x * w, img.y * omw + target.y * w, img.z * omw + target.z * w,
-                              img.w * omw + target.w * w);
-            alb = make_float4(alb.x * omw + ta.x * w, alb.y * omw + ta.y * w, alb.z * omw + ta.z * w, 0.0f);
-            nrm = make_float4(nrm.x * omw + tn.x * w, nrm.y * omw + tn.y * w, nrm.z * omw + tn.z * w, 0.0f);
+            const bool hit = st.flags & F_HIT;
+            const bool env = !hit && !P.envhidden && S.nenvs != 0;
+            const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
+            // no bounce-0 surface was accepted: st.d is still the camera ray direction
+            if (!hit) aov_update(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
+            float4 img = A.image[pixel];
+            A.image[pixel] = make_float4(img.x * omw + target.x * w, img.y * omw + target.y * w,
+                                         img.z * omw + target.z * w, img.w * omw + target.w * w);
+            if (hit || env) A.hits[pixel] += 1;
             if (++sample >= s_end) break;
+            aov.w = 1.0f / (float)(sample - P.first + 1);
             start_path(P, i, j, pixel, sample, st);
         }
-        A.image[pixel] = img;
-        A.albedo[pixel] = alb;
-        A.normal[pixel] = nrm;
-        A.hits[pixel] = hits;
     }
     // one atomic per counter per wave
-    unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims, cnt.shades};
+    unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
+                     COUNT ? cnt.shades : 0u};
 #pragma unroll
     for (int k = 0; k < 7; k++) {
         unsigned s = wave_sum(v[k]);
@@ -699,19 +730,19 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
     }
 }
 
-template <int SAMPLER, int STACK>
+template <int SAMPLER, int STACK, int COUNT>
 hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st) {
     dim3 grid((P.width + 15) / 16, (P.height + 15) / 16);
-    hipLaunchKernelGGL((trace_kernel<SAMPLER, STACK>), grid, dim3(BLOCK), 0, st, S, P, s0, s1, A);
+    hipLaunchKernelGGL((trace_kernel<SAMPLER, STACK, COUNT>), grid, dim3(BLOCK), 0, st, S, P, s0, s1, A);
     return hipGetLastError();
 }
 
-template <int SAMPLER>
+template <int SAMPLER, int COUNT>
 hipError_t launch_s(int stack, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st) {
-    if (stack <= 16) return launch_t<SAMPLER, 16>(S, P, s0, s1, A, st);
-    if (stack <= 32) return launch_t<SAMPLER, 32>(S, P, s0, s1, A, st);
-    if (stack <= 64) return launch_t<SAMPLER, 64>(S, P, s0, s1, A, st);
-    return launch_t<SAMPLER, 128>(S, P, s0, s1, A, st);
+    if (stack <= 16) return launch_t<SAMPLER, 16, COUNT>(S, P, s0, s1, A, st);
+    if (stack <= 32) return launch_t<SAMPLER, 32, COUNT>(S, P, s0, s1, A, st);
+    if (stack <= 64) return launch_t<SAMPLER, 64, COUNT>(S, P, s0, s1, A, st);
+    return launch_t<SAMPLER, 128, COUNT>(S, P, s0, s1, A, st);
 }
 
 }  // namespace
@@ -728,6 +759,7 @@ struct jt_ctx {
     int width = 0, height = 0;
     int total_samples = 0, batch = 1, sampler = 1, stack = 16;
     int first = -1, next = 0;  // running-mean origin and next expected sample
+    int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     unsigned long long launches = 0;
     double kernel_ms = 0;
 };
@@ -1175,8 +1207,12 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     (void)hipSetDevice(c->device);
     hipError_t e = hipEventRecord(c->ev0, c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
-    e = c->sampler == JT_SAMPLER_NAIVE ? launch_s<2>(c->stack, c->S, c->P, s0, s1, c->A, c->stream)
-                                       : launch_s<1>(c->stack, c->S, c->P, s0, s1, c->A, c->stream);
+    if (c->sampler == JT_SAMPLER_NAIVE)
+        e = c->count ? launch_s<2, 1>(c->stack, c->S, c->P, s0, s1, c->A, c->stream)
+                     : launch_s<2, 0>(c->stack, c->S, c->P, s0, s1, c->A, c->stream);
+    else
+        e = c->count ? launch_s<1, 1>(c->stack, c->S, c->P, s0, s1, c->A, c->stream)
+                     : launch_s<1, 0>(c->stack, c->S, c->P, s0, s1, c->A, c->stream);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipEventSynchronize(c->ev1)) != hipSuccess) return hip_fail(e, "trace kernel");
@@ -1271,6 +1307,13 @@ int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
     out->width = c->width;
     out->height = c->height;
     out->stream = c->stream;
+    return JT_OK;
+}
+
+int jt_set_counters(jt_ctx* c, int32_t level) {
+    if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    if (level != 0 && level != 1) return jt::fail(JT_ERR_INVALID, "counter level must be 0 or 1");
+    c->count = level;
     return JT_OK;
 }
 

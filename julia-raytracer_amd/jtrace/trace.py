@@ -136,6 +136,9 @@ class TraceState:
         abi.check(self.lib, self.lib.jt_get_device_buffers(self.handle, C.byref(b)))
         return b
 
+    def set_counters(self, level: int):
+        abi.check(self.lib, self.lib.jt_set_counters(self.handle, int(level)))
+
     def reset(self):
         abi.check(self.lib, self.lib.jt_reset(self.handle))
 
