@@ -123,7 +123,7 @@ __device__ __forceinline__ v4 eval_texture(const DScene& S, int tex, v2 uv, bool
     return ((a + b) + c) + d;
 }
 // eval_normalmap (src/scene.jl:722-751) with eval_element_tangents (:851-891)
-__device__ __noinline__ v3 eval_normalmap(const DScene& S, const DShape& sh, const int4& e, const fr3& f,
+__device__ __forceinline__ v3 eval_normalmap(const DScene& S, const DShape& sh, const int4& e, const fr3& f,
                                           const DMaterial& m, v2 uv) {
     v3 normal = eval_normal(S, sh, e, f, uv);
     v2 texcoord = eval_texcoord(S, sh, e, uv);
@@ -215,7 +215,7 @@ __device__ __forceinline__ void eval_shading(const DScene& S, int inst, int elem
 }
 
 // eval_environment (src/scene.jl:893-914)
-__device__ __noinline__ v3 eval_environment(const DScene& S, v3 direction) {
+__device__ __forceinline__ v3 eval_environment(const DScene& S, v3 direction) {
     v3 emission = V3(0, 0, 0);
     for (int k = 0; k < S.nenvs; k++) {
         const DEnv& env = S.envs[k];
@@ -354,7 +354,7 @@ __device__ __forceinline__ v3 sample_lights(const DScene& S, v3 position, float 
     return V3(0, 0, 0);
 }
 // env-light term of sample_lights_pdf (src/trace.jl:1045-1079)
-__device__ __noinline__ float env_light_pdf(const DScene& S, const DLight l, v3 direction) {
+__device__ __forceinline__ float env_light_pdf(const DScene& S, const DLight l, v3 direction) {
     const float* cdf = S.cdf + l.cdf_offset;
     const DEnv& env = S.envs[l.environment];
     const DTexture t = S.textures[env.tex];
