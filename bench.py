@@ -109,7 +109,8 @@ def main():
     lights = trace.make_trace_lights(sa, lib)
     state = trace.make_trace_state(sa, bvh, lights, jp, lib)
     W, H, S = state.width, state.height, args.spp
-    s0, s1 = rank * S // world, (rank + 1) * S // world
+    from jtrace.parallel import reduce_running_means, shard_range
+    s0, s1 = shard_range(S, world, rank)
 
     img_t = None
     if world > 1:
@@ -123,11 +124,8 @@ def main():
     def step():
         state.reset()
         state.trace_range(s0, s1)
-        if world > 1:
-            part = img_t * float(s1 - s0)  # sample-weighted running mean of this shard
-            dist.reduce(part, dst=0, op=dist.ReduceOp.SUM)
-            if rank == 0:
-                part /= float(S)
+        if world > 1:  # the path's one exchange: sum of sample-weighted shard means (RCCL)
+            reduce_running_means(img_t, s1 - s0, S, dist, dst=0)
         return state.counters()
 
     for _ in range(args.warmup):

@@ -100,7 +100,7 @@ struct DParams {
     float clamp;
     int envhidden, tentfilter, nocaustics;
     int first;  // running-mean origin: weight of sample s is 1/(s - first + 1)
-    int pad;
+    int wait_lanes;
     unsigned long long seed;
 };
 

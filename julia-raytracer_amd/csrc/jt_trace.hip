@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -244,87 +245,108 @@ struct Counters {
     unsigned rays, light_queries, nodes, instances, prims, shades, paths;
 };
 
-// One traversal loop for intersect_scene_bvh (root = TLAS node 0) and intersect_instance_bvh
-// (root = one instance entry). Closest hit; a primitive with t == tmax replaces the current hit,
-// exactly as the reference's `t > ray.tmax -> reject` test in the reference's visit order.
-template <int COUNT>
-__device__ __forceinline__ Hit traverse(const DScene& S, v3 wo, v3 wd, unsigned root, int* stack, Counters& cnt) {
-    Hit h{-1, -1, 0, 0, 0, false};
-    float tmax = __builtin_inff();
-    const float tmin = ray_eps;
-    const v3 wdinv = V3(1 / wd.x, 1 / wd.y, 1 / wd.z);
-    v3 lo = wo, ld = wd, ldinv = wdinv;
-    int cur_inst = -1, cur_kind = KIND_TRI;
-    int sp = 0;
+// A resumable BVH query per lane, for intersect_scene_bvh (root = TLAS node 0) and
+// intersect_instance_bvh (root = one instance entry). query_step() does one unit of work: one
+// node (box test + push), one instance entry (ray to instance space), or ONE primitive test of
+// the current leaf (leaf cursor), so every step costs about the same whatever a lane is doing.
+// Visit order — children far-first per d[axis] sign, a TLAS leaf's instances in order, a BLAS
+// leaf's primitives in order before anything else is popped — is exactly the reference's, so
+// the closest hit and its tie-breaking (t == tmax replaces; only t > tmax rejects) match.
+struct Trav {
+    v3 wo, wd, wdinv;  // world-space ray of the query
+    v3 lo, ld, ldinv;  // ray in the current instance's space (transform_ray, src/geometry.jl:107)
+    float tmax;
+    int sp;            // LDS stack entries
+    int cur_inst, cur_kind;
+    int prim, nprim;   // leaf cursor: next primitive record, primitives left
+    Hit h;
+};
+
+__device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T.nprim > 0; }
+
+__device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, int* stack) {
+    T.wo = o;
+    T.wd = d;
+    T.wdinv = V3(1 / d.x, 1 / d.y, 1 / d.z);  // ray_dinv (src/bvh.jl:322), no guard
+    T.lo = o;
+    T.ld = d;
+    T.ldinv = T.wdinv;
+    T.tmax = __builtin_inff();
+    T.h = Hit{-1, -1, 0, 0, 0, false};
+    T.nprim = 0;
+    T.prim = 0;
+    T.cur_inst = -1;
+    T.cur_kind = KIND_TRI;
     stack[0] = (int)root;
-    sp = 1;
-    while (sp > 0) {
-        sp--;
-        const unsigned e = (unsigned)stack[sp * BLOCK];
-        const unsigned type = e >> 30, idx = e & IDX_MASK;
-        if (type == T_INST) {
-            // instance visit: inverse(frame, true) precomputed on the host (src/bvh.jl:345,502)
-            const DInstTrav it = S.inst_trav[idx];
-            if (COUNT) cnt.instances++;
-            const fr3 inv = frame_from(it.i0, it.i1, it.i2);
-            lo = transform_point(inv, wo);
-            ld = transform_vector(inv, wd);
-            ldinv = V3(1 / ld.x, 1 / ld.y, 1 / ld.z);
-            cur_inst = (int)idx;
-            cur_kind = it.kind;
-            stack[sp * BLOCK] = (int)((T_BLAS << 30) | (unsigned)it.blas_root);
-            sp++;
-            continue;
-        }
-        const bool blas = type == T_BLAS;
-        const DNode nd = blas ? S.blas_nodes[idx] : S.tlas_nodes[idx];
-        if (COUNT) cnt.nodes++;
-        const v3 o = blas ? lo : wo;
-        const v3 dv = blas ? ldinv : wdinv;
-        if (!intersect_bbox(o, dv, tmin, tmax, nd.a, nd.b)) continue;
-        const unsigned meta = __float_as_uint(nd.b.w);
-        const int start = __float_as_int(nd.a.w);
-        const int num = (int)(meta & 0xffffu);
-        if (meta >> 24) {  // internal: children start, start+1; far child first for d[axis] >= 0
-            const int axis = (int)((meta >> 16) & 0xffu);
-            const v3 d = blas ? ld : wd;
-            const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-            const unsigned tag = type << 30;
-            const int first = da < 0 ? start + 1 : start;
-            const int second = da < 0 ? start : start + 1;
-            stack[sp * BLOCK] = (int)(tag | (unsigned)first);
-            stack[(sp + 1) * BLOCK] = (int)(tag | (unsigned)second);
-            sp += 2;
-        } else if (!blas) {  // TLAS leaf: instances in order start .. start+num-1
-            for (int k = num - 1; k >= 0; k--) {
-                stack[sp * BLOCK] = (int)((T_INST << 30) | (unsigned)S.tlas_prims[start + k]);
-                sp++;
-            }
-        } else if (cur_kind == KIND_TRI) {
-            for (int k = 0; k < num; k++) {
-                const float4* r = S.prims + 3 * (start + k);
-                const float4 a = r[0], b = r[1], c = r[2];
-                if (COUNT) cnt.prims++;
-                PrimHit p = intersect_triangle(lo, ld, tmin, tmax, xyz(a), xyz(b), xyz(c));
-                if (p.hit) {
-                    h = Hit{cur_inst, __float_as_int(a.w), p.u, p.v, p.t, true};
-                    tmax = p.t;
-                }
-            }
+    T.sp = 1;
+}
+
+template <int COUNT>
+__device__ __forceinline__ void query_step(const DScene& S, Trav& T, int* stack, Counters& cnt) {
+    const float tmin = ray_eps;
+    if (T.nprim > 0) {  // one primitive of the current BLAS leaf (src/bvh.jl:444-484)
+        if (COUNT) cnt.prims++;
+        PrimHit p;
+        int elem;
+        if (T.cur_kind == KIND_TRI) {
+            const float4* r = S.prims + 3 * T.prim;
+            const float4 a = r[0], b = r[1], c = r[2];
+            elem = __float_as_int(a.w);
+            p = intersect_triangle(T.lo, T.ld, tmin, T.tmax, xyz(a), xyz(b), xyz(c));
         } else {
-            for (int k = 0; k < num; k++) {
-                const float4* r = S.prims + 4 * (start + k);
-                const float4 a = r[0], b = r[1], c = r[2], d = r[3];
-                if (COUNT) cnt.prims++;
-                PrimHit p = intersect_quad(lo, ld, tmin, tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
-                if (p.hit) {
-                    h = Hit{cur_inst, __float_as_int(a.w), p.u, p.v, p.t, true};
-                    tmax = p.t;
-                }
-            }
+            const float4* r = S.prims + 4 * T.prim;
+            const float4 a = r[0], b = r[1], c = r[2], d = r[3];
+            elem = __float_as_int(a.w);
+            p = intersect_quad(T.lo, T.ld, tmin, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
         }
+        if (p.hit) {
+            T.h = Hit{T.cur_inst, elem, p.u, p.v, p.t, true};
+            T.tmax = p.t;
+        }
+        T.prim += 1;
+        T.nprim -= 1;
+        return;
     }
-    return h;
+    T.sp -= 1;
+    const unsigned e = (unsigned)stack[T.sp * BLOCK];
+    const unsigned type = e >> 30, idx = e & IDX_MASK;
+    if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
+        if (COUNT) cnt.instances++;
+        const DInstTrav it = S.inst_trav[idx];
+        const fr3 inv = frame_from(it.i0, it.i1, it.i2);
+        T.lo = transform_point(inv, T.wo);
+        T.ld = transform_vector(inv, T.wd);
+        T.ldinv = V3(1 / T.ld.x, 1 / T.ld.y, 1 / T.ld.z);
+        T.cur_inst = (int)idx;
+        T.cur_kind = it.kind;
+        stack[T.sp * BLOCK] = (int)((T_BLAS << 30) | (unsigned)it.blas_root);
+        T.sp += 1;
+        return;
+    }
+    const bool blas = type == T_BLAS;
+    const DNode nd = blas ? S.blas_nodes[idx] : S.tlas_nodes[idx];
+    if (COUNT) cnt.nodes++;
+    if (!intersect_bbox(blas ? T.lo : T.wo, blas ? T.ldinv : T.wdinv, tmin, T.tmax, nd.a, nd.b)) return;
+    const unsigned meta = __float_as_uint(nd.b.w);
+    const int start = __float_as_int(nd.a.w);
+    const int num = (int)(meta & 0xffffu);
+    if (meta >> 24) {  // internal: for d[axis] >= 0 push start, start+1 (start+1 pops first)
+        const int axis = (int)((meta >> 16) & 0xffu);
+        const v3 d = blas ? T.ld : T.wd;
+        const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+        const unsigned tag = type << 30;
+        stack[T.sp * BLOCK] = (int)(tag | (unsigned)(da < 0 ? start + 1 : start));
+        stack[(T.sp + 1) * BLOCK] = (int)(tag | (unsigned)(da < 0 ? start : start + 1));
+        T.sp += 2;
+    } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
+        for (int k = num - 1; k >= 0; k--) {
+            stack[T.sp * BLOCK] = (int)((T_INST << 30) | (unsigned)S.tlas_prims[start + k]);
+            T.sp += 1;
+        }
+    } else {  // BLAS leaf: its primitives are tested next, in order
+        T.prim = start;
+        T.nprim = num;
+    }
 }
 
 // ============================================================================ lights (src/trace.jl)
@@ -371,9 +393,9 @@ __device__ __forceinline__ float env_light_pdf(const DScene& S, const DLight l, 
 
 // ============================================================================ integrator
 // trace_path / trace_naive restated as a per-lane state machine. Every iteration of the
-// kernel's loop issues exactly one BVH query per lane — a closest-hit scene query (PH_SCENE)
-// or one intersect_instance_bvh query of sample_lights_pdf (PH_LIGHT) — through the single
-// `traverse` call site, then advances the lane's state. Float operations and RNG draws happen
+// kernel's shading phase issues exactly one BVH query per waiting lane — a closest-hit scene
+// query (PH_SCENE) or one intersect_instance_bvh query of sample_lights_pdf (PH_LIGHT) —
+// which the traversal phase then advances (query_step). Float operations and RNG draws happen
 // in exactly the reference's order; only where the lane waits between them changes.
 enum : int { PH_SCENE = 0, PH_LIGHT = 1 };
 enum : int { F_HIT = 1, F_VOLUME = 2 };
@@ -680,45 +702,71 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
     const int i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int j = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    if (i < P.width && j < P.height && s_begin < s_end) {
-        const int pixel = j * P.width + i;
-        int sample = s_begin;
-        Aov aov{A.albedo, A.normal, pixel, 1.0f / (float)(sample - P.first + 1)};
-        Path st;
+    const int pixel = j * P.width + i;
+    bool alive = i < P.width && j < P.height && s_begin < s_end;
+    int sample = s_begin;
+    Aov aov{A.albedo, A.normal, pixel, 1.0f / (float)(sample - P.first + 1)};
+    Path st;
+    Trav T;
+    T.sp = 0;
+    T.nprim = 0;
+    if (alive) {
         start_path(P, i, j, pixel, sample, st);
+        cnt.rays++;
+        query_begin(T, st.o, st.d, T_TLAS << 30, stack);
+    }
+    for (;;) {
+        // traversal phase: step every lane with a query in flight until at least W lanes wait
         for (;;) {
-            const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
-            const v3 qo = light ? st.lq : st.o;
-            const unsigned root = light ? ((T_INST << 30) | (unsigned)S.lights[st.li].instance) : (T_TLAS << 30);
-            if (light) cnt.light_queries++;
-            else cnt.rays++;
-            const Hit h = traverse<COUNT>(S, qo, st.d, root, stack, cnt);
-            bool done;
-            if (light) done = light_hit(S, P, st, h);
-            else if (SAMPLER == 2) done = naive_hit(S, P, st, h, aov, cnt.shades);
-            else done = path_hit(S, P, st, h, aov, cnt.shades);
-            if (!done) continue;
-            // trace_sample epilogue (src/trace.jl:625-648)
-            cnt.paths++;
-            v3 radiance = st.radiance;
-            if (!all_finite(radiance)) radiance = V3(0, 0, 0);
-            const float mr = max3(radiance);
-            if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
-            const float w = aov.w;
-            const float omw = 1 - w;
-            const bool hit = st.flags & F_HIT;
-            const bool env = !hit && !P.envhidden && S.nenvs != 0;
-            const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
-            // no bounce-0 surface was accepted: st.d is still the camera ray direction
-            if (!hit) aov_update(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
-            float4 img = A.image[pixel];
-            A.image[pixel] = make_float4(img.x * omw + target.x * w, img.y * omw + target.y * w,
-                                         img.z * omw + target.z * w, img.w * omw + target.w * w);
-            if (hit || env) A.hits[pixel] += 1;
-            if (++sample >= s_end) break;
-            aov.w = 1.0f / (float)(sample - P.first + 1);
-            start_path(P, i, j, pixel, sample, st);
+            const bool busy = alive && query_busy(T);
+            const int nb = __popcll(__ballot(busy));
+            const int nw = __popcll(__ballot(alive && !busy));
+            if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
+            if (busy) query_step<COUNT>(S, T, stack, cnt);
         }
+        // shading phase: every waiting lane consumes its hit and issues its next query
+        if (alive && !query_busy(T)) {
+            const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
+            bool done;
+            if (light) done = light_hit(S, P, st, T.h);
+            else if (SAMPLER == 2) done = naive_hit(S, P, st, T.h, aov, cnt.shades);
+            else done = path_hit(S, P, st, T.h, aov, cnt.shades);
+            if (done) {
+                // trace_sample epilogue (src/trace.jl:625-648)
+                cnt.paths++;
+                v3 radiance = st.radiance;
+                if (!all_finite(radiance)) radiance = V3(0, 0, 0);
+                const float mr = max3(radiance);
+                if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
+                const float w = aov.w;
+                const float omw = 1 - w;
+                const bool hit = st.flags & F_HIT;
+                const bool env = !hit && !P.envhidden && S.nenvs != 0;
+                const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
+                // no bounce-0 surface was accepted: st.d is still the camera ray direction
+                if (!hit) aov_update(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
+                float4 img = A.image[pixel];
+                A.image[pixel] = make_float4(img.x * omw + target.x * w, img.y * omw + target.y * w,
+                                             img.z * omw + target.z * w, img.w * omw + target.w * w);
+                if (hit || env) A.hits[pixel] += 1;
+                if (++sample >= s_end) {
+                    alive = false;
+                } else {
+                    aov.w = 1.0f / (float)(sample - P.first + 1);
+                    start_path(P, i, j, pixel, sample, st);
+                }
+            }
+            if (alive) {
+                if (SAMPLER == 1 && st.phase == PH_LIGHT) {
+                    cnt.light_queries++;
+                    query_begin(T, st.lq, st.d, (T_INST << 30) | (unsigned)S.lights[st.li].instance, stack);
+                } else {
+                    cnt.rays++;
+                    query_begin(T, st.o, st.d, T_TLAS << 30, stack);
+                }
+            }
+        }
+        if (__ballot(alive) == 0) break;
     }
     // one atomic per counter per wave
     unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
@@ -1156,6 +1204,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.nocaustics = params->nocaustics;
     P.first = 0;
     P.seed = params->seed;
+    // lanes that must be waiting before a shading phase runs; tunable
+    P.wait_lanes = 32;
+    if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
 
     // accumulators (make_trace_state: zeroed) + counters
     const size_t np = (size_t)W * (size_t)H;
