@@ -68,6 +68,7 @@ struct DScene {
     const DNode* blas_nodes;
     const float4* prims;  // triangle: 3 float4 (p1|elem, p2, p3); quad: 4 float4 (p4.w = p3==p4)
     const DInstTrav* inst_trav;
+    const int4* inst_blas;  // per instance: blas_root, kind, identity-transform flag, shape
     const DInstShade* inst_shade;
     const DShape* shapes;
     const float4* pos;

@@ -246,7 +246,7 @@ struct Counters {
 };
 
 // A resumable BVH query per lane, for intersect_scene_bvh (root = TLAS node 0) and
-// intersect_instance_bvh (root = one instance entry). query_step() does one unit of work: one
+// intersect_instance_bvh (root = one instance entry). node_step() / prim_step() do one unit of work: one
 // node (box test + push), one instance entry (ray to instance space), or ONE primitive test of
 // the current leaf (leaf cursor), so every step costs about the same whatever a lane is doing.
 // Visit order — children far-first per d[axis] sign, a TLAS leaf's instances in order, a BLAS
@@ -281,52 +281,62 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     T.sp = 1;
 }
 
+// One primitive of the current BLAS leaf (src/bvh.jl:444-484).
 template <int COUNT>
-__device__ __forceinline__ void query_step(const DScene& S, Trav& T, int* stack, Counters& cnt) {
-    const float tmin = ray_eps;
-    if (T.nprim > 0) {  // one primitive of the current BLAS leaf (src/bvh.jl:444-484)
-        if (COUNT) cnt.prims++;
-        PrimHit p;
-        int elem;
-        if (T.cur_kind == KIND_TRI) {
-            const float4* r = S.prims + 3 * T.prim;
-            const float4 a = r[0], b = r[1], c = r[2];
-            elem = __float_as_int(a.w);
-            p = intersect_triangle(T.lo, T.ld, tmin, T.tmax, xyz(a), xyz(b), xyz(c));
-        } else {
-            const float4* r = S.prims + 4 * T.prim;
-            const float4 a = r[0], b = r[1], c = r[2], d = r[3];
-            elem = __float_as_int(a.w);
-            p = intersect_quad(T.lo, T.ld, tmin, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
-        }
-        if (p.hit) {
-            T.h = Hit{T.cur_inst, elem, p.u, p.v, p.t, true};
-            T.tmax = p.t;
-        }
-        T.prim += 1;
-        T.nprim -= 1;
-        return;
+__device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cnt) {
+    if (COUNT) cnt.prims++;
+    PrimHit p;
+    int elem;
+    if (T.cur_kind == KIND_TRI) {
+        const float4* r = S.prims + 3 * T.prim;
+        const float4 a = r[0], b = r[1], c = r[2];
+        elem = __float_as_int(a.w);
+        p = intersect_triangle(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c));
+    } else {
+        const float4* r = S.prims + 4 * T.prim;
+        const float4 a = r[0], b = r[1], c = r[2], d = r[3];
+        elem = __float_as_int(a.w);
+        p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
     }
+    if (p.hit) {
+        T.h = Hit{T.cur_inst, elem, p.u, p.v, p.t, true};
+        T.tmax = p.t;
+    }
+    T.prim += 1;
+    T.nprim -= 1;
+}
+
+// Pop one stack entry: an instance entry or a TLAS/BLAS node.
+template <int COUNT>
+__device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, Counters& cnt) {
     T.sp -= 1;
     const unsigned e = (unsigned)stack[T.sp * BLOCK];
     const unsigned type = e >> 30, idx = e & IDX_MASK;
     if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
         if (COUNT) cnt.instances++;
-        const DInstTrav it = S.inst_trav[idx];
-        const fr3 inv = frame_from(it.i0, it.i1, it.i2);
-        T.lo = transform_point(inv, T.wo);
-        T.ld = transform_vector(inv, T.wd);
-        T.ldinv = V3(1 / T.ld.x, 1 / T.ld.y, 1 / T.ld.z);
+        const int4 ib = S.inst_blas[idx];  // blas_root, kind, identity, shape
+        if (ib.z) {
+            // inverse(identity) is exactly the identity: transform_ray returns the ray bit for bit
+            T.lo = T.wo;
+            T.ld = T.wd;
+            T.ldinv = T.wdinv;
+        } else {
+            const DInstTrav it = S.inst_trav[idx];
+            const fr3 inv = frame_from(it.i0, it.i1, it.i2);
+            T.lo = transform_point(inv, T.wo);
+            T.ld = transform_vector(inv, T.wd);
+            T.ldinv = V3(1 / T.ld.x, 1 / T.ld.y, 1 / T.ld.z);
+        }
         T.cur_inst = (int)idx;
-        T.cur_kind = it.kind;
-        stack[T.sp * BLOCK] = (int)((T_BLAS << 30) | (unsigned)it.blas_root);
+        T.cur_kind = ib.y;
+        stack[T.sp * BLOCK] = (int)((T_BLAS << 30) | (unsigned)ib.x);
         T.sp += 1;
         return;
     }
     const bool blas = type == T_BLAS;
     const DNode nd = blas ? S.blas_nodes[idx] : S.tlas_nodes[idx];
     if (COUNT) cnt.nodes++;
-    if (!intersect_bbox(blas ? T.lo : T.wo, blas ? T.ldinv : T.wdinv, tmin, T.tmax, nd.a, nd.b)) return;
+    if (!intersect_bbox(blas ? T.lo : T.wo, blas ? T.ldinv : T.wdinv, ray_eps, T.tmax, nd.a, nd.b)) return;
     const unsigned meta = __float_as_uint(nd.b.w);
     const int start = __float_as_int(nd.a.w);
     const int num = (int)(meta & 0xffffu);
@@ -343,7 +353,7 @@ __device__ __forceinline__ void query_step(const DScene& S, Trav& T, int* stack,
             stack[T.sp * BLOCK] = (int)((T_INST << 30) | (unsigned)S.tlas_prims[start + k]);
             T.sp += 1;
         }
-    } else {  // BLAS leaf: its primitives are tested next, in order
+    } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
     }
@@ -395,7 +405,7 @@ __device__ __forceinline__ float env_light_pdf(const DScene& S, const DLight l, 
 // trace_path / trace_naive restated as a per-lane state machine. Every iteration of the
 // kernel's shading phase issues exactly one BVH query per waiting lane — a closest-hit scene
 // query (PH_SCENE) or one intersect_instance_bvh query of sample_lights_pdf (PH_LIGHT) —
-// which the traversal phase then advances (query_step). Float operations and RNG draws happen
+// which the traversal phase then advances (node_step / prim_step). Float operations and RNG draws happen
 // in exactly the reference's order; only where the lane waits between them changes.
 enum : int { PH_SCENE = 0, PH_LIGHT = 1 };
 enum : int { F_HIT = 1, F_VOLUME = 2 };
@@ -717,12 +727,22 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
     }
     for (;;) {
         // traversal phase: step every lane with a query in flight until at least W lanes wait
+        // Each iteration runs ONE step kind — primitive tests or stack pops — picked by lane
+        // majority (a wave-uniform branch), so the SIMD executes one code path per iteration.
+        // A lane's own sequence of steps is unchanged: it only waits while the other kind runs.
         for (;;) {
-            const bool busy = alive && query_busy(T);
-            const int nb = __popcll(__ballot(busy));
-            const int nw = __popcll(__ballot(alive && !busy));
+            const bool wantp = alive && T.nprim > 0;
+            const bool wantn = alive && T.nprim == 0 && T.sp > 0;
+            const int np = __popcll(__ballot(wantp));
+            const int nn = __popcll(__ballot(wantn));
+            const int nw = __popcll(__ballot(alive && !wantp && !wantn));
+            const int nb = np + nn;
             if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
-            if (busy) query_step<COUNT>(S, T, stack, cnt);
+            if (np >= nn) {
+                if (wantp) prim_step<COUNT>(S, T, cnt);
+            } else {
+                if (wantn) node_step<COUNT>(S, T, stack, cnt);
+            }
         }
         // shading phase: every waiting lane consumes its hit and issues its next query
         if (alive && !query_busy(T)) {
@@ -1090,6 +1110,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         }
     }
     std::vector<DInstTrav> itrav(scene->ninstances);
+    std::vector<int4> iblas(scene->ninstances);
     std::vector<DInstShade> ishade(scene->ninstances);
     for (int k = 0; k < scene->ninstances; k++) {
         const jt_instance& in = scene->instances[k];
@@ -1101,6 +1122,12 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         const DShape& d = shapes[in.shape];
         itrav[k] = DInstTrav{f4(iv[0], iv[1], iv[2], iv[3]), f4(iv[4], iv[5], iv[6], iv[7]), f4(iv[8], iv[9], iv[10], iv[11]),
                              in.shape, d.blas_root, d.kind, d.prim_base};
+        // identity inverse (exact 1/0 entries, zero offset): transform_ray is the identity on
+        // floats, so the traversal reuses the world ray (bit-identical)
+        const float idm[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+        bool ident = true;
+        for (int q = 0; q < 12; q++) ident = ident && iv[q] == idm[q];
+        iblas[k] = make_int4(d.blas_root, d.kind, ident ? 1 : 0, in.shape);
         ishade[k] = DInstShade{f4(fv[0], fv[1], fv[2], fv[3]), f4(fv[4], fv[5], fv[6], fv[7]), f4(fv[8], fv[9], fv[10], fv[11]),
                                in.material, in.shape, scene->materials[in.material].type, 0};
     }
@@ -1174,7 +1201,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     DScene& S = c->S;
     if ((st = upload(c, tlas, &S.tlas_nodes)) || (st = upload(c, tlas_prims, &S.tlas_prims)) ||
         (st = upload(c, blas, &S.blas_nodes)) || (st = upload(c, prims, &S.prims)) ||
-        (st = upload(c, itrav, &S.inst_trav)) || (st = upload(c, ishade, &S.inst_shade)) ||
+        (st = upload(c, itrav, &S.inst_trav)) || (st = upload(c, iblas, &S.inst_blas)) || (st = upload(c, ishade, &S.inst_shade)) ||
         (st = upload(c, shapes, &S.shapes)) || (st = upload(c, pos, &S.pos)) || (st = upload(c, nrm, &S.nrm)) ||
         (st = upload(c, tc, &S.tc)) || (st = upload(c, col, &S.col)) || (st = upload(c, elems, &S.elems)) ||
         (st = upload(c, mats, &S.materials)) || (st = upload(c, texs, &S.textures)) || (st = upload(c, texb, &S.texb)) ||
