@@ -86,6 +86,13 @@ struct DScene {
     const float* srgb_lut;  // srgb_to_rgb(byte_to_float(b)), 256 entries (src/color.jl:12-23)
     const float* byte_lut;  // byte_to_float(b)
     int tlas_nnodes, nenvs, nlights, pad;
+    // Small-scene mode: every array above that the traversal and shading read per step, packed
+    // in one 16-B aligned blob the workgroup copies into LDS at kernel start (offsets in 16-B
+    // units; -1 = not in the blob). Texels, environments and LUTs stay in HBM.
+    const uint4* blob;
+    int blob_n16;
+    int o_tlas_nodes, o_tlas_prims, o_blas_nodes, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
+    int o_pos, o_nrm, o_tc, o_col, o_elems, o_materials, o_lights, o_cdf;
 };
 
 struct DCamera {

@@ -26,6 +26,10 @@
 #include "jt_device.h"
 #include "jt_internal.h"
 
+#ifndef JT_STAMPS
+#define JT_STAMPS 0
+#endif
+
 using namespace jtd;
 
 namespace {
@@ -705,9 +709,8 @@ struct DAccum {
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
 // mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
 template <int SAMPLER, int STACK, int COUNT>
-__global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
-    __shared__ int lds_stack[STACK * BLOCK];
-    int* stack = lds_stack + threadIdx.x;
+__device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
+                                           int* stack) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int j = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
@@ -725,7 +728,13 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
         cnt.rays++;
         query_begin(T, st.o, st.d, T_TLAS << 30, stack);
     }
+#if JT_STAMPS
+    unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
+#endif
     for (;;) {
+#if JT_STAMPS
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
         // traversal phase: step every lane with a query in flight until at least W lanes wait
         // Each iteration runs ONE step kind — primitive tests or stack pops — picked by lane
         // majority (a wave-uniform branch), so the SIMD executes one code path per iteration.
@@ -738,12 +747,21 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
             const int nw = __popcll(__ballot(alive && !wantp && !wantn));
             const int nb = np + nn;
             if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
+#if JT_STAMPS
+            n_trav++;
+            if (np >= nn) { steps_p++; lanes_p += np; } else { steps_n++; lanes_n += nn; }
+#endif
             if (np >= nn) {
                 if (wantp) prim_step<COUNT>(S, T, cnt);
             } else {
                 if (wantn) node_step<COUNT>(S, T, stack, cnt);
             }
         }
+#if JT_STAMPS
+        unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        t_trav += t1 - t0;
+        n_shade++;
+#endif
         // shading phase: every waiting lane consumes its hit and issues its next query
         if (alive && !query_busy(T)) {
             const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
@@ -786,8 +804,24 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
                 }
             }
         }
+#if JT_STAMPS
+        t_shade += __builtin_amdgcn_s_memtime() - t1;
+#endif
         if (__ballot(alive) == 0) break;
     }
+#if JT_STAMPS
+    if (lane == 0) {
+        unsigned long long* dbg = A.counters + 8;
+        atomicAdd(dbg + 0, t_trav);
+        atomicAdd(dbg + 1, t_shade);
+        atomicAdd(dbg + 2, n_trav);
+        atomicAdd(dbg + 3, n_shade);
+        atomicAdd(dbg + 4, lanes_p);
+        atomicAdd(dbg + 5, lanes_n);
+        atomicAdd(dbg + 6, steps_p);
+        atomicAdd(dbg + 7, steps_n);
+    }
+#endif
     // one atomic per counter per wave
     unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
                      COUNT ? cnt.shades : 0u};
@@ -798,10 +832,54 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
     }
 }
 
+// HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS.
+template <int SAMPLER, int STACK, int COUNT>
+__global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
+    __shared__ int lds_stack[STACK * BLOCK];
+    trace_body<SAMPLER, STACK, COUNT>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
+}
+
+// LDS mode (small scenes): the workgroup stages the scene blob into LDS once; every node,
+// instance, primitive and shading record is then a ds_read instead of a vector-memory load
+// through the TA/TD path (the measured limiter of the HBM-mode kernel).
+template <int SAMPLER, int STACK, int COUNT>
+__global__ __launch_bounds__(BLOCK) void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
+    extern __shared__ uint4 dyn_lds[];
+    uint4* blob = dyn_lds + (STACK * BLOCK) / 4;
+    for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
+    __syncthreads();
+    DScene L = S;
+    L.tlas_nodes = reinterpret_cast<const DNode*>(blob + S.o_tlas_nodes);
+    L.tlas_prims = reinterpret_cast<const int*>(blob + S.o_tlas_prims);
+    L.blas_nodes = reinterpret_cast<const DNode*>(blob + S.o_blas_nodes);
+    L.prims = reinterpret_cast<const float4*>(blob + S.o_prims);
+    L.inst_trav = reinterpret_cast<const DInstTrav*>(blob + S.o_inst_trav);
+    L.inst_blas = reinterpret_cast<const int4*>(blob + S.o_inst_blas);
+    L.inst_shade = reinterpret_cast<const DInstShade*>(blob + S.o_inst_shade);
+    L.shapes = reinterpret_cast<const DShape*>(blob + S.o_shapes);
+    L.pos = reinterpret_cast<const float4*>(blob + S.o_pos);
+    L.nrm = reinterpret_cast<const float4*>(blob + S.o_nrm);
+    L.tc = reinterpret_cast<const float2*>(blob + S.o_tc);
+    L.col = reinterpret_cast<const float4*>(blob + S.o_col);
+    L.elems = reinterpret_cast<const int4*>(blob + S.o_elems);
+    L.materials = reinterpret_cast<const DMaterial*>(blob + S.o_materials);
+    L.lights = reinterpret_cast<const DLight*>(blob + S.o_lights);
+    L.cdf = reinterpret_cast<const float*>(blob + S.o_cdf);
+    trace_body<SAMPLER, STACK, COUNT>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+}
+
 template <int SAMPLER, int STACK, int COUNT>
 hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st) {
     dim3 grid((P.width + 15) / 16, (P.height + 15) / 16);
-    hipLaunchKernelGGL((trace_kernel<SAMPLER, STACK, COUNT>), grid, dim3(BLOCK), 0, st, S, P, s0, s1, A);
+    if (S.blob_n16 > 0) {
+        const size_t lds = (size_t)STACK * BLOCK * 4 + (size_t)S.blob_n16 * 16;
+        hipError_t e = hipFuncSetAttribute((const void*)trace_kernel_lds<SAMPLER, STACK, COUNT>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, STACK, COUNT>), grid, dim3(BLOCK), lds, st, S, P, s0, s1, A);
+    } else {
+        hipLaunchKernelGGL((trace_kernel<SAMPLER, STACK, COUNT>), grid, dim3(BLOCK), 0, st, S, P, s0, s1, A);
+    }
     return hipGetLastError();
 }
 
@@ -828,6 +906,7 @@ struct jt_ctx {
     int total_samples = 0, batch = 1, sampler = 1, stack = 16;
     int first = -1, next = 0;  // running-mean origin and next expected sample
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
+    size_t lds_scene_bytes = 0;  // > 0: small-scene LDS mode
     unsigned long long launches = 0;
     double kernel_ms = 0;
 };
@@ -1212,6 +1291,49 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     S.nenvs = scene->nenvironments;
     S.nlights = lights->nlights;
 
+    // ------------------------------------------------------------- small-scene LDS blob
+    {
+        std::vector<uint4> blob;
+        auto add = [&](const void* data, size_t bytes) {
+            const int off = (int)blob.size();
+            const size_t n16 = (bytes + 15) / 16;
+            blob.resize(blob.size() + std::max<size_t>(1, n16));
+            if (bytes) std::memcpy(blob.data() + off, data, bytes);
+            return off;
+        };
+        S.o_tlas_nodes = add(tlas.data(), tlas.size() * sizeof(DNode));
+        S.o_tlas_prims = add(tlas_prims.data(), tlas_prims.size() * sizeof(int));
+        S.o_blas_nodes = add(blas.data(), blas.size() * sizeof(DNode));
+        S.o_prims = add(prims.data(), prims.size() * sizeof(float4));
+        S.o_inst_trav = add(itrav.data(), itrav.size() * sizeof(DInstTrav));
+        S.o_inst_blas = add(iblas.data(), iblas.size() * sizeof(int4));
+        S.o_inst_shade = add(ishade.data(), ishade.size() * sizeof(DInstShade));
+        S.o_shapes = add(shapes.data(), shapes.size() * sizeof(DShape));
+        S.o_pos = add(pos.data(), pos.size() * sizeof(float4));
+        S.o_nrm = add(nrm.data(), nrm.size() * sizeof(float4));
+        S.o_tc = add(tc.data(), tc.size() * sizeof(float2));
+        S.o_col = add(col.data(), col.size() * sizeof(float4));
+        S.o_elems = add(elems.data(), elems.size() * sizeof(int4));
+        S.o_materials = add(mats.data(), mats.size() * sizeof(DMaterial));
+        S.o_lights = add(dl.data(), dl.size() * sizeof(DLight));
+        S.o_cdf = add(cdf.data(), cdf.size() * sizeof(float));
+        // budget: the blob plus the stack of the chosen STACK size must leave room for >= 2
+        // workgroups per CU (160 KiB LDS); override with JT_LDS_SCENE=0 (off) or a byte budget
+        size_t budget = 48 * 1024;
+        if (const char* v = std::getenv("JT_LDS_SCENE")) budget = (size_t)std::atoll(v);
+        const int stack_entries = c->stack <= 16 ? 16 : c->stack <= 32 ? 32 : c->stack <= 64 ? 64 : 128;
+        const size_t stack_bytes = (size_t)stack_entries * 256 * 4;
+        const size_t bytes = blob.size() * 16;
+        S.blob = nullptr;
+        S.blob_n16 = 0;
+        if (bytes <= budget && bytes + stack_bytes <= 80 * 1024) {
+            std::vector<uint4> b(blob);
+            if ((st = upload(c, b, &S.blob))) return bail(st);
+            S.blob_n16 = (int)blob.size();
+        }
+        c->lds_scene_bytes = S.blob_n16 ? bytes : 0;
+    }
+
     DParams& P = c->P;
     const jt_camera& cam = scene->cameras[params->camera];
     std::memcpy(P.cam.frame, cam.frame, sizeof(P.cam.frame));
@@ -1246,7 +1368,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     c->allocations.push_back(nrmb);
     if ((e = hipMalloc(&hits, np * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc accumulators"));
     c->allocations.push_back(hits);
-    if ((e = hipMalloc(&cnt, 8 * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc counters"));
+    if ((e = hipMalloc(&cnt, 16 * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc counters"));
     c->allocations.push_back(cnt);
     c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt};
     st = jt_reset(c);
@@ -1264,7 +1386,7 @@ int jt_reset(jt_ctx* c) {
         (e = hipMemsetAsync(c->A.albedo, 0, np * 16, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->A.normal, 0, np * 16, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->A.hits, 0, np * 8, c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->A.counters, 0, 64, c->stream)) != hipSuccess)
+        (e = hipMemsetAsync(c->A.counters, 0, 128, c->stream)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync");
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     c->first = -1;
@@ -1386,6 +1508,13 @@ int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
     out->height = c->height;
     out->stream = c->stream;
     return JT_OK;
+}
+
+// diagnostic build only (JT_STAMPS=1): per-phase wave clocks, read by scripts/stamps.py
+extern "C" int jt_debug_stamps(jt_ctx* c, unsigned long long* out8) {
+    if (!c || !out8) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    hipError_t e = hipMemcpy(out8, c->A.counters + 8, 8 * 8, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy stamps");
 }
 
 int jt_set_counters(jt_ctx* c, int32_t level) {

@@ -1,0 +1,32 @@
+"""Diagnostic: run the bench workload on the JT_STAMPS build and print the traversal/shading
+split of wave time and step-lane utilisation (never used for timed numbers)."""
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+os.environ["JTRACE_LIB"] = str(ROOT / "julia-raytracer_amd" / "build" / "libjtrace_hip_stamps.so")
+sys.path.insert(0, str(ROOT / "julia-raytracer_amd"))
+from jtrace import abi, sceneio, trace  # noqa: E402
+from jtrace.cli import Params  # noqa: E402
+
+spp = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+lib = abi.load_library()
+lib.jt_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+scene = sceneio.load_scene(str(ROOT / "assets/scenes/cornellbox/cornellbox.json"))
+sa = abi.SceneABI(scene)
+jp = abi.make_params(Params(scene="", samples=spp, width=1280, height=720, batch=spp), 0)
+st = trace.make_trace_state(sa, trace.make_scene_bvh(sa, False, lib), trace.make_trace_lights(sa, lib), jp, lib)
+st.set_counters(0)
+st.trace_range(0, spp)
+v = (C.c_ulonglong * 8)()
+abi.check(lib, lib.jt_debug_stamps(st.handle, v))
+t_trav, t_shade, n_trav, n_shade, lanes_p, lanes_n, steps_p, steps_n = list(v)
+tot = t_trav + t_shade
+print(f"wait_lanes={os.environ.get('JT_WAIT_LANES', 32)} spp={spp} kernel_ms={st.counters()['kernel_ms']:.1f}")
+print(f"traversal phase {t_trav / tot:.1%}  shading phase {t_shade / tot:.1%}")
+print(f"trav iterations/wave-shade-phase {n_trav / max(1, n_shade):.2f}; cycles per trav iter {t_trav / max(1, n_trav):.0f}; "
+      f"cycles per shading phase {t_shade / max(1, n_shade):.0f}")
+print(f"prim steps {steps_p} (avg lanes {lanes_p / max(1, steps_p):.1f}), node steps {steps_n} "
+      f"(avg lanes {lanes_n / max(1, steps_n):.1f})")

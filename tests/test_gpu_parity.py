@@ -120,3 +120,24 @@ def test_statistical_pin_full_resolution(gpu, abi, lib, cornell_abi):
     print("block rel err median", np.median(rel), "p95", np.percentile(rel, 95))
     assert np.median(rel) < 0.03
     assert np.percentile(rel, 95) < 0.15
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
+def test_lds_and_hbm_scene_modes_bitwise_equal(gpu, abi, lib, cornell_abi, sampler, monkeypatch):
+    """The small-scene LDS mode and the HBM mode run the same program on the same data."""
+    from jtrace import trace
+    bvh = trace.make_scene_bvh(cornell_abi, False, lib)
+    lights = trace.make_trace_lights(cornell_abi, lib)
+    p = make_params(abi, resolution=80, samples=4, sampler=sampler)
+    imgs = []
+    for mode in ("0", "65536"):
+        monkeypatch.setenv("JT_LDS_SCENE", mode)
+        st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
+        st.trace_range(0, 4)
+        imgs.append((st.get_image(), st.get_aovs(), st.counters()))
+        st.close()
+    assert np.array_equal(imgs[0][0], imgs[1][0])
+    for a, b in zip(imgs[0][1], imgs[1][1]):
+        assert np.array_equal(a, b)
+    for k in ("rays", "light_queries", "nodes", "instances", "prims", "shades"):
+        assert imgs[0][2][k] == imgs[1][2][k], k
