@@ -1132,6 +1132,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         d.kind = sh.ntriangles ? KIND_TRI : KIND_QUAD;
         const int stride = d.kind == KIND_TRI ? 3 : 4;
         d.blas_root = (int)blas.size();
+        // records are 3 (triangle) or 4 (quad) float4s: align the shape's first record to its
+        // stride so prim_base * stride addresses it exactly when shape kinds are mixed
+        while (prims.size() % stride) prims.push_back(f4(0, 0, 0, 0));
         d.prim_base = (int)(prims.size() / stride);  // in records
         d.idx_base = (int)elems.size();
         d.pos_base = (int)pos.size();
@@ -1354,7 +1357,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.first = 0;
     P.seed = params->seed;
     // lanes that must be waiting before a shading phase runs; tunable
-    P.wait_lanes = 32;
+    P.wait_lanes = 48;
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
 
     // accumulators (make_trace_state: zeroed) + counters

@@ -1,0 +1,128 @@
+"""HIP path vs the oracle on the reference's feature scenes, and the statistical pin of the HIP
+path against the reference's own renders of them (images/<scene>_<sampler>.png, block means
+committed in tests/golden/scene_pins.npz by tests/golden/scripts/make_scene_pins.py).
+
+Scene coverage of SURVEY.md §8(a):
+  features1  glossy/refractive/reflective, normal map (A22), HDR env light (A9/A10/A23), quads
+  features2  config 3 (hairball/displacedsubdiv missing in the reference checkout: dropped)
+  materials1 glossy + rough/delta reflective (A26/A27)
+  materials2 refractive + transparent (A28/A29)
+  materials4 volumetric + refractive with a volume stack (A11/A30)
+  shapes1    quads of several BLAS shapes, textured matte/glossy
+Tolerance as tests/test_gpu_parity.py (>= 99.9 % of pixels within 1e-3 relative; image mean
+within 1e-4 relative).
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, compare_images, make_params
+
+pytestmark = pytest.mark.gpu
+
+SCENES = ("features1", "features2", "materials1", "materials2", "materials4", "shapes1")
+_cache = {}
+
+
+def scene_abi(name):
+    if name not in _cache:
+        import warnings
+        from jtrace import abi, sceneio
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            sc = sceneio.load_scene(str(ROOT / "assets" / "scenes" / name / f"{name}.json"), missing="drop")
+        _cache[name] = abi.SceneABI(sc)
+    return _cache[name]
+
+
+def render_gpu(lib, sa, params, s0, s1, high_quality=False):
+    from jtrace import trace
+    bvh = trace.make_scene_bvh(sa, high_quality, lib)
+    lights = trace.make_trace_lights(sa, lib)
+    st = trace.make_trace_state(sa, bvh, lights, params, lib)
+    st.trace_range(s0, s1)
+    out = (st.get_image(), *st.get_aovs(), st.counters())
+    st.close()
+    return out
+
+
+def render_oracle(oracle, sa, params, W, H, s0, s1, high_quality=False):
+    ob = oracle.build_bvh(sa, high_quality)
+    ol = oracle.make_lights(sa)
+    return oracle.trace(sa, ob, ol, params, W, H, s0, s1)
+
+
+def check_parity(g, o, label):
+    stats = compare_images(g[0], o[0])
+    print(label, stats, "gpu rays", g[4]["rays"], "oracle rays", o[4]["rays"])
+    assert stats["frac_pix_rel_le_1e-3"] >= 0.999, (label, stats)
+    assert stats["image_mean_rel"] <= 1e-4, (label, stats)
+    assert np.array_equal(g[3], o[3]), label  # hit counts
+    for k in ("rays", "light_queries", "nodes", "instances", "prims", "shades"):
+        assert abs(g[4][k] - o[4][k]) <= 1e-3 * o[4][k] + 8, (label, k, g[4][k], o[4][k])
+    for a, b in ((g[1], o[1]), (g[2], o[2])):
+        s = compare_images(a, b)
+        assert s["frac_pix_rel_le_1e-3"] >= 0.999, (label, s)
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
+@pytest.mark.parametrize("name", SCENES)
+def test_scene_parity(gpu, abi, lib, oracle, name, sampler):
+    sa = scene_abi(name)
+    p = make_params(abi, resolution=120, samples=6, sampler=sampler)
+    g = render_gpu(lib, sa, p, 0, 6)
+    o = render_oracle(oracle, sa, p, g[0].shape[1], g[0].shape[0], 0, 6)
+    check_parity(g, o, f"{name}/{sampler}")
+
+
+@pytest.mark.parametrize("flags", [
+    dict(tentfilter=True), dict(nocaustics=True), dict(envhidden=True), dict(clamp=2),
+    dict(bounces=2), dict(bounces=16, sampler=2)])
+def test_param_variants_parity(gpu, abi, lib, oracle, flags):
+    name = "materials2" if "nocaustics" in flags else "features1"
+    sa = scene_abi(name)
+    p = make_params(abi, resolution=96, samples=4, **flags)
+    g = render_gpu(lib, sa, p, 0, 4)
+    o = render_oracle(oracle, sa, p, g[0].shape[1], g[0].shape[0], 0, 4)
+    check_parity(g, o, f"{name}/{flags}")
+
+
+def test_high_quality_bvh_parity(gpu, abi, lib, oracle):
+    """--highqualitybvh (SAH build, src/bvh.jl:223-304): same host build on both sides."""
+    sa = scene_abi("shapes1")
+    p = make_params(abi, resolution=96, samples=4)
+    g = render_gpu(lib, sa, p, 0, 4, high_quality=True)
+    o = render_oracle(oracle, sa, p, g[0].shape[1], g[0].shape[0], 0, 4, high_quality=True)
+    check_parity(g, o, "shapes1/sah")
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
+@pytest.mark.parametrize("name", SCENES)
+def test_statistical_pin_reference_render(gpu, abi, lib, name, sampler):
+    """HIP render at the reference's size (1280x533), 128 spp (naive: 1024), through the sRGB + 8-bit
+    pipeline, vs the reference's own PNG on 41x40-pixel block means (this also pins the HDR
+    decode, sceneio.HDR_MODE). features2's reference render holds two shapes the checkout
+    lacks (hairball, displacedsubdiv): looser channel-mean and median bounds, no p95 bound."""
+    from jtrace import sceneio
+    pins = np.load(Path(__file__).parent / "golden" / "scene_pins.npz")
+    key = f"{name}_{'path' if sampler == 1 else 'naive'}"
+    w, h = (int(v) for v in pins[key + "_size"])
+    bh, bw = (int(v) for v in pins["block"])
+    sa = scene_abi(name)
+    spp = 128 if sampler == 1 else 1024  # the naive sampler is far noisier; the 8-bit sRGB
+    p = make_params(abi, resolution=1280, samples=spp, sampler=sampler, batch=spp)  # mean is
+    img = render_gpu(lib, sa, p, 0, spp)[0]  # biased low by noise (concave encode)
+    assert img.shape[:2] == (h, w)
+    lin = sceneio.decode_srgb8(sceneio.to_srgb8(img, w, h))[..., :3]
+    bm = lin.reshape(h // bh, bh, w // bw, bw, 3).mean(axis=(1, 3))
+    ref = pins[key + "_mean"]
+    cm = lin.reshape(-1, 3).mean(axis=0)
+    rel = np.abs(bm - ref) / np.maximum(ref, 0.02)
+    print(key, "channel mean", cm, "reference", pins[key + "_channel_mean"],
+          "block rel median", np.median(rel), "p95", np.percentile(rel, 95))
+    f2 = name == "features2"
+    np.testing.assert_allclose(cm, pins[key + "_channel_mean"], rtol=0.05 if f2 else 0.01)
+    assert np.median(rel) < (0.02 if f2 else 0.01)
+    if not f2:
+        assert np.percentile(rel, 95) < 0.04

@@ -63,6 +63,11 @@ def test_hdr_rle_roundtrip_and_clamp(tmp_path):
     np.testing.assert_allclose(got, ref.astype(np.float32))
     t = sceneio.load_texture(str(f))
     assert t.linear and t.pixelsf.max() <= 1.0 and np.all(t.pixelsf[..., 3] == 1)
+    # default decode: clamp, sRGB-encode, 16-bit quantise (sceneio.HDR_MODE)
+    c = np.clip(ref, 0, 1)
+    enc = np.where(c <= 0.0031308, 12.92 * c, 1.055 * c ** (1 / 2.4) - 0.055)
+    np.testing.assert_allclose(t.pixelsf[..., :3], np.round(enc * 65535) / 65535, atol=1e-7)
+    np.testing.assert_array_equal(sceneio.load_texture(str(f), "clamp").pixelsf[..., :3], c.astype(np.float32))
 
 
 def test_png_rgb_alpha_is_one_byte(tmp_path):
