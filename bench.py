@@ -52,6 +52,20 @@ def shade_record_bytes(scene) -> int:
     return best
 
 
+def pmc_traffic(workload: str, kernel: str):
+    """HBM bytes per launch of `kernel` on `workload` from the committed rocprofv3 PMC summary
+    (profiles/*_traffic.json, written by scripts/pmc_traffic.py from separate --pmc passes of
+    this same bench command); None when no summary matches."""
+    for f in sorted((ROOT / "profiles").glob("*_traffic.json"), reverse=True):
+        try:
+            d = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload and d.get("kernel", "").replace(" ", "") == kernel:
+            return d["traffic"], f.name
+    return None, None
+
+
 def cpu_baseline(scene_abi, params, width, height, nthreads, spp=2):
     """Oracle (C restatement, oracle/jt_oracle.c) on host cores: bounded sample of the same
     workload — all pixels, samples [0, spp)."""
@@ -81,7 +95,7 @@ def main():
     ap.add_argument("--scene", default=str(ROOT / "assets" / "scenes" / "cornellbox" / "cornellbox.json"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-spp", type=int, default=32)
+    ap.add_argument("--cpu-spp", type=int, default=128)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,6 +150,8 @@ def main():
     state.set_counters(1)
     full = step()
     state.set_counters(0)
+    desc = state.describe()
+    kernel = desc.split()[0].split("=", 1)[1]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -173,9 +189,12 @@ def main():
         bytes_per_launch = algorithmic_bytes(per_launch, shade_record_bytes(scene),
                                              any(len(s.quads) for s in scene.shapes))
         achieved = bytes_per_launch / avg_launch_s / 1e9
+        workload = f"{Path(args.scene).stem} {args.sampler} {W}x{H} {s1 - s0} samples/launch"
+        traffic, traffic_src = pmc_traffic(workload, kernel)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "trace_kernel<1,16,0>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
+                "kernel": kernel, "launch": desc, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                 "bytes_per_launch": int(bytes_per_launch),
                 "bytes_per_ray": round(bytes_per_launch / max(1.0, per_launch["rays"]), 1)}
         cpu = None

@@ -274,6 +274,10 @@ int jt_get_device_buffers(jt_ctx* ctx, jt_device_buffers* out);
  * paths, rays and light_queries only (the timed production kernel; the other fields are
  * deterministic given seed + BVH and are taken from a level-1 launch of the same range). */
 int jt_set_counters(jt_ctx* ctx, int32_t level);
+/* NUL-terminated one-line description of the launch configuration the next jt_trace_range
+ * uses (kernel instance, LDS/HBM scene mode, stack depth, grid): names the kernel in
+ * rocprofv3 traces. Truncated to n bytes. */
+int jt_describe(const jt_ctx* ctx, char* buf, int32_t n);
 int jt_synchronize(jt_ctx* ctx);
 void jt_destroy(jt_ctx* ctx);
 

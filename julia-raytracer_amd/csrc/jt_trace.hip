@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -1518,6 +1519,19 @@ extern "C" int jt_debug_stamps(jt_ctx* c, unsigned long long* out8) {
     if (!c || !out8) return jt::fail(JT_ERR_INVALID, "NULL argument");
     hipError_t e = hipMemcpy(out8, c->A.counters + 8, 8 * 8, hipMemcpyDeviceToHost);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy stamps");
+}
+
+int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
+    if (!c || !buf || n <= 0) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    const int stack = c->stack <= 16 ? 16 : c->stack <= 32 ? 32 : c->stack <= 64 ? 64 : 128;
+    char tmp[512];
+    std::snprintf(tmp, sizeof tmp,
+                  "kernel=%s<%d,%d,%d> mode=%s scene_lds_bytes=%zu stack=%d wait_lanes=%d grid=%dx%d block=%d",
+                  c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
+                  stack, c->count, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes, stack, c->P.wait_lanes,
+                  (c->width + 15) / 16, (c->height + 15) / 16, BLOCK);
+    std::snprintf(buf, (size_t)n, "%s", tmp);
+    return JT_OK;
 }
 
 int jt_set_counters(jt_ctx* c, int32_t level) {

@@ -269,6 +269,7 @@ def _declare(lib):
     lib.jt_get_device_buffers.argtypes = [C.c_void_p, C.POINTER(jt_device_buffers)]
     lib.jt_set_counters.argtypes = [C.c_void_p, C.c_int32]
     lib.jt_synchronize.argtypes = [C.c_void_p]
+    lib.jt_describe.argtypes = [C.c_void_p, C.c_char_p, C.c_int32]
     lib.jt_destroy.argtypes = [C.c_void_p]
     lib.jt_destroy.restype = None
     return lib
@@ -279,7 +280,7 @@ EXPORTED_SYMBOLS = [
     "jt_version", "jt_abi_version", "jt_last_error", "jt_device_count", "jt_build_scene_bvh",
     "jt_free_scene_bvh", "jt_make_lights", "jt_free_lights", "jt_image_size", "jt_create",
     "jt_trace_samples", "jt_trace_range", "jt_get_samples", "jt_get_size", "jt_get_image",
-    "jt_get_aovs", "jt_get_counters", "jt_reset", "jt_get_device_buffers", "jt_set_counters", "jt_synchronize",
+    "jt_get_aovs", "jt_get_counters", "jt_reset", "jt_get_device_buffers", "jt_set_counters", "jt_describe", "jt_synchronize",
     "jt_destroy",
 ]
 

@@ -139,6 +139,12 @@ class TraceState:
     def set_counters(self, level: int):
         abi.check(self.lib, self.lib.jt_set_counters(self.handle, int(level)))
 
+    def describe(self) -> str:
+        """Launch configuration of the next trace_range (kernel instance, scene mode, grid)."""
+        buf = C.create_string_buffer(512)
+        abi.check(self.lib, self.lib.jt_describe(self.handle, buf, 512))
+        return buf.value.decode()
+
     def reset(self):
         abi.check(self.lib, self.lib.jt_reset(self.handle))
 
