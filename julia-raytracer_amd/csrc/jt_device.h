@@ -380,21 +380,42 @@ __device__ __forceinline__ v2 sample_triangle(v2 ruv) {  // :58
 }
 
 // ------------------------------------------------------------------------------ geometry.jl
+// Raw VALU min/max. Only for operands known not to be NaN: the compiler's fminf/fmaxf
+// canonicalize both inputs first (IEEE mode), which costs an extra VALU op per operand.
+__device__ __forceinline__ float vmin(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // intersect_bbox (src/geometry.jl:96-105): Julia min/max; `t1 *= 1.00000024` is Float64.
+// Any NaN slab value makes Julia's t0 or t1 NaN and culls the box; that case is tested
+// separately, so the min/max chains below only ever see non-NaN values, where IEEE min/max
+// agree with Julia's (signed zeros cannot change `t0 <= t1`) and the order of the chain does
+// not matter.
 __device__ __forceinline__ bool intersect_bbox(v3 o, v3 dinv, float tmin, float tmax, const float4& a,
                                                const float4& b) {
     float mx = (a.x - o.x) * dinv.x, my = (a.y - o.y) * dinv.y, mz = (a.z - o.z) * dinv.z;
     float Mx = (b.x - o.x) * dinv.x, My = (b.y - o.y) * dinv.y, Mz = (b.z - o.z) * dinv.z;
-    // equivalent to the Julia min/max chains: any NaN slab value culls (t0 or t1 is NaN), and
-    // signed zeros cannot change `t0 <= t1`; otherwise IEEE min/max agree with Julia's.
     bool nan = __builtin_isnan(mx) | __builtin_isnan(my) | __builtin_isnan(mz) | __builtin_isnan(Mx) |
                __builtin_isnan(My) | __builtin_isnan(Mz);
-    float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(mx, Mx), __builtin_fminf(my, My)),
-                                               __builtin_fminf(mz, Mz)),
-                               tmin);
-    float t1 = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fmaxf(mx, Mx), __builtin_fmaxf(my, My)),
-                                               __builtin_fmaxf(mz, Mz)),
-                               tmax);
+    float t0 = vmax3(vmin(mx, Mx), vmin(my, My), vmax(vmin(mz, Mz), tmin));
+    float t1 = vmin3(vmax(mx, Mx), vmax(my, My), vmin(vmax(mz, Mz), tmax));
     return !nan && ((double)t0 <= (double)t1 * 1.00000024);
 }
 
@@ -402,35 +423,43 @@ struct PrimHit {
     float u, v, t;
     bool hit;
 };
-// intersect_triangle (src/geometry.jl:206-236)
+// intersect_triangle (src/geometry.jl:206-236), branchless: every quantity is computed and the
+// reference's early-out tests are combined into one predicate (the same comparisons, so NaN
+// behaves as in the reference: a NaN u, v or t fails none of them). A miss is (0, 0, inf).
 __device__ __forceinline__ PrimHit intersect_triangle(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 p2, v3 p3) {
-    PrimHit miss{0, 0, __builtin_inff(), false};
     v3 edge1 = p2 - p1, edge2 = p3 - p1;
     v3 pvec = cross(d, edge2);
     float det = dot(edge1, pvec);
-    if (det == 0) return miss;
     float inv_det = 1.0f / det;
     v3 tvec = o - p1;
     float u = dot(tvec, pvec) * inv_det;
-    if (u < 0 || u > 1) return miss;
     v3 qvec = cross(tvec, edge1);
     float v = dot(d, qvec) * inv_det;
-    if (v < 0 || u + v > 1) return miss;
     float t = dot(edge2, qvec) * inv_det;
-    if (t < tmin || t > tmax) return miss;
-    return PrimHit{u, v, t, true};
+    const bool miss = (det == 0) | (u < 0 || u > 1) | (v < 0 || u + v > 1) | (t < tmin || t > tmax);
+    PrimHit r;
+    r.u = miss ? 0.0f : u;
+    r.v = miss ? 0.0f : v;
+    r.t = miss ? __builtin_inff() : t;
+    r.hit = !miss;
+    return r;
 }
 // intersect_quad (src/geometry.jl:238-258); `degenerate` = (p3 == p4), precomputed on the host
 __device__ __forceinline__ PrimHit intersect_quad(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 p2, v3 p3, v3 p4,
                                                   bool degenerate) {
-    if (degenerate) return intersect_triangle(o, d, tmin, tmax, p1, p2, p4);
     PrimHit i1 = intersect_triangle(o, d, tmin, tmax, p1, p2, p4);
     PrimHit i2 = intersect_triangle(o, d, tmin, tmax, p3, p4, p2);
     if (i2.hit) {
         i2.u = 1 - i2.u;
         i2.v = 1 - i2.v;
     }
-    return i1.t < i2.t ? i1 : i2;
+    const bool first = degenerate || i1.t < i2.t;
+    PrimHit r;
+    r.u = first ? i1.u : i2.u;
+    r.v = first ? i1.v : i2.v;
+    r.t = first ? i1.t : i2.t;
+    r.hit = first ? i1.hit : i2.hit;
+    return r;
 }
 __device__ __forceinline__ v3 triangle_normal(v3 p1, v3 p2, v3 p3) { return normalize(cross(p2 - p1, p3 - p1)); }
 __device__ __forceinline__ v3 quad_normal(v3 p1, v3 p2, v3 p3, v3 p4) {

@@ -259,13 +259,26 @@ struct Counters {
 // the closest hit and its tie-breaking (t == tmax replaces; only t > tmax rejects) match.
 struct Trav {
     v3 wo, wd, wdinv;  // world-space ray of the query
-    v3 lo, ld, ldinv;  // ray in the current instance's space (transform_ray, src/geometry.jl:107)
+    v3 lo, ld, ldinv;  // the ray every node test uses: the world ray, or inside a BLAS the ray
+                       // in the current instance's space (transform_ray, src/geometry.jl:107)
     float tmax;
     int sp;            // LDS stack entries
+    int inst_space;    // lo/ld/ldinv hold an instance-space ray (restore before a TLAS pop)
+    int negmask;       // bit a set <=> ld[a] < 0 (the push order of src/bvh.jl:331-341, 424-434)
     int cur_inst, cur_kind;
     int prim, nprim;   // leaf cursor: next primitive record, primitives left
     Hit h;
 };
+
+__device__ __forceinline__ int neg_mask(v3 d) { return (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0); }
+
+__device__ __forceinline__ void world_ray(Trav& T) {
+    T.lo = T.wo;
+    T.ld = T.wd;
+    T.ldinv = T.wdinv;
+    T.negmask = neg_mask(T.wd);
+    T.inst_space = 0;
+}
 
 __device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T.nprim > 0; }
 
@@ -282,6 +295,8 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     T.prim = 0;
     T.cur_inst = -1;
     T.cur_kind = KIND_TRI;
+    T.inst_space = 0;
+    T.negmask = neg_mask(d);
     stack[0] = (int)root;
     T.sp = 1;
 }
@@ -322,15 +337,15 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         const int4 ib = S.inst_blas[idx];  // blas_root, kind, identity, shape
         if (ib.z) {
             // inverse(identity) is exactly the identity: transform_ray returns the ray bit for bit
-            T.lo = T.wo;
-            T.ld = T.wd;
-            T.ldinv = T.wdinv;
+            if (T.inst_space) world_ray(T);
         } else {
             const DInstTrav it = S.inst_trav[idx];
             const fr3 inv = frame_from(it.i0, it.i1, it.i2);
             T.lo = transform_point(inv, T.wo);
             T.ld = transform_vector(inv, T.wd);
             T.ldinv = V3(1 / T.ld.x, 1 / T.ld.y, 1 / T.ld.z);
+            T.negmask = neg_mask(T.ld);
+            T.inst_space = 1;
         }
         T.cur_inst = (int)idx;
         T.cur_kind = ib.y;
@@ -339,19 +354,19 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         return;
     }
     const bool blas = type == T_BLAS;
+    if (!blas && T.inst_space) world_ray(T);  // back from an instance: TLAS nodes test the world ray
     const DNode nd = blas ? S.blas_nodes[idx] : S.tlas_nodes[idx];
     if (COUNT) cnt.nodes++;
-    if (!intersect_bbox(blas ? T.lo : T.wo, blas ? T.ldinv : T.wdinv, ray_eps, T.tmax, nd.a, nd.b)) return;
+    if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
     const unsigned meta = __float_as_uint(nd.b.w);
     const int start = __float_as_int(nd.a.w);
     const int num = (int)(meta & 0xffffu);
     if (meta >> 24) {  // internal: for d[axis] >= 0 push start, start+1 (start+1 pops first)
         const int axis = (int)((meta >> 16) & 0xffu);
-        const v3 d = blas ? T.ld : T.wd;
-        const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+        const bool neg = (T.negmask >> axis) & 1;  // d[axis] < 0
         const unsigned tag = type << 30;
-        stack[T.sp * BLOCK] = (int)(tag | (unsigned)(da < 0 ? start + 1 : start));
-        stack[(T.sp + 1) * BLOCK] = (int)(tag | (unsigned)(da < 0 ? start : start + 1));
+        stack[T.sp * BLOCK] = (int)(tag | (unsigned)(neg ? start + 1 : start));
+        stack[(T.sp + 1) * BLOCK] = (int)(tag | (unsigned)(neg ? start : start + 1));
         T.sp += 2;
     } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
         for (int k = num - 1; k >= 0; k--) {
@@ -833,9 +848,19 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     }
 }
 
+// Occupancy request (waves per SIMD); JT_WAVES=0 leaves it to the compiler.
+#ifndef JT_WAVES
+#define JT_WAVES 0
+#endif
+#if JT_WAVES > 0
+#define JT_WAVES_PER_EU __attribute__((amdgpu_waves_per_eu(JT_WAVES, JT_WAVES)))
+#else
+#define JT_WAVES_PER_EU
+#endif
+
 // HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS.
 template <int SAMPLER, int STACK, int COUNT>
-__global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
+__global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     __shared__ int lds_stack[STACK * BLOCK];
     trace_body<SAMPLER, STACK, COUNT>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
 }
@@ -844,7 +869,7 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(DScene S, DParams P, int s
 // instance, primitive and shading record is then a ds_read instead of a vector-memory load
 // through the TA/TD path (the measured limiter of the HBM-mode kernel).
 template <int SAMPLER, int STACK, int COUNT>
-__global__ __launch_bounds__(BLOCK) void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
+__global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     extern __shared__ uint4 dyn_lds[];
     uint4* blob = dyn_lds + (STACK * BLOCK) / 4;
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
@@ -886,10 +911,15 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
 
 template <int SAMPLER, int COUNT>
 hipError_t launch_s(int stack, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st) {
+#if JT_ONE_VARIANT  // compile-time experiments only (make quick-usage): one kernel instance
+    (void)stack;
+    return launch_t<1, 16, 0>(S, P, s0, s1, A, st);
+#else
     if (stack <= 16) return launch_t<SAMPLER, 16, COUNT>(S, P, s0, s1, A, st);
     if (stack <= 32) return launch_t<SAMPLER, 32, COUNT>(S, P, s0, s1, A, st);
     if (stack <= 64) return launch_t<SAMPLER, 64, COUNT>(S, P, s0, s1, A, st);
     return launch_t<SAMPLER, 128, COUNT>(S, P, s0, s1, A, st);
+#endif
 }
 
 }  // namespace
