@@ -506,17 +506,24 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
 // trace_path's bounce body after the closest-hit query (src/trace.jl:298-453)
 // The albedo/normal running means (src/trace.jl:635-636) are updated as soon as the bounce-0
 // surface is accepted — their targets are final at that point — so they are not path state.
+// Per-lane running means of the lane's pixel, kept in LDS for the whole launch (a lane owns
+// its pixel for all its samples): acc[k * BLOCK], k = 0..3 image rgba, 4..6 albedo, 7..9
+// normal, 10 hit count of this launch (int). Loaded from / stored to HBM once per launch; the
+// per-sample lerps are the same float operations as a read-modify-write of the HBM buffers.
+constexpr int ACC_SLOTS = 11;
 struct Aov {
-    float4* albedo;
-    float4* normal;
-    int pixel;
+    float* acc;
     float w;
 };
 __device__ __forceinline__ void aov_update(const Aov& a, v3 ta, v3 tn) {
     const float omw = 1 - a.w;
-    float4 alb = a.albedo[a.pixel], nrm = a.normal[a.pixel];
-    a.albedo[a.pixel] = make_float4(alb.x * omw + ta.x * a.w, alb.y * omw + ta.y * a.w, alb.z * omw + ta.z * a.w, 0.0f);
-    a.normal[a.pixel] = make_float4(nrm.x * omw + tn.x * a.w, nrm.y * omw + tn.y * a.w, nrm.z * omw + tn.z * a.w, 0.0f);
+    float* p = a.acc;
+    p[4 * BLOCK] = p[4 * BLOCK] * omw + ta.x * a.w;
+    p[5 * BLOCK] = p[5 * BLOCK] * omw + ta.y * a.w;
+    p[6 * BLOCK] = p[6 * BLOCK] * omw + ta.z * a.w;
+    p[7 * BLOCK] = p[7 * BLOCK] * omw + tn.x * a.w;
+    p[8 * BLOCK] = p[8 * BLOCK] * omw + tn.y * a.w;
+    p[9 * BLOCK] = p[9 * BLOCK] * omw + tn.z * a.w;
 }
 
 __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const Aov& aov,
@@ -732,9 +739,26 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     const int j = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     const int pixel = j * P.width + i;
-    bool alive = i < P.width && j < P.height && s_begin < s_end;
+    const bool in_image = i < P.width && j < P.height;
+    bool alive = in_image && s_begin < s_end;
     int sample = s_begin;
-    Aov aov{A.albedo, A.normal, pixel, 1.0f / (float)(sample - P.first + 1)};
+    __shared__ float acc_lds[ACC_SLOTS * BLOCK];
+    float* acc = acc_lds + threadIdx.x;
+    if (in_image) {
+        const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
+        acc[0] = im.x;
+        acc[BLOCK] = im.y;
+        acc[2 * BLOCK] = im.z;
+        acc[3 * BLOCK] = im.w;
+        acc[4 * BLOCK] = al.x;
+        acc[5 * BLOCK] = al.y;
+        acc[6 * BLOCK] = al.z;
+        acc[7 * BLOCK] = nr.x;
+        acc[8 * BLOCK] = nr.y;
+        acc[9 * BLOCK] = nr.z;
+        reinterpret_cast<int*>(acc)[10 * BLOCK] = 0;
+    }
+    Aov aov{acc, 1.0f / (float)(sample - P.first + 1)};
     Path st;
     Trav T;
     T.sp = 0;
@@ -746,6 +770,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     }
 #if JT_STAMPS
     unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
+    unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
 #endif
     for (;;) {
 #if JT_STAMPS
@@ -782,9 +807,23 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         if (alive && !query_busy(T)) {
             const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
             bool done;
+#if JT_STAMPS
+            unsigned long long s0 = __builtin_amdgcn_s_memtime();
+            if (light) done = light_hit(S, P, st, T.h);
+            unsigned long long s1 = __builtin_amdgcn_s_memtime();
+            if (!light) {
+                if (SAMPLER == 2) done = naive_hit(S, P, st, T.h, aov, cnt.shades);
+                else done = path_hit(S, P, st, T.h, aov, cnt.shades);
+            }
+            unsigned long long s2 = __builtin_amdgcn_s_memtime();
+            if (__ballot(light)) { t_lhit += s1 - s0; n_lhit++; }
+            if (__ballot(!light)) { t_phit += s2 - s1; n_phit++; }
+            if (__ballot(done)) n_fin++;
+#else
             if (light) done = light_hit(S, P, st, T.h);
             else if (SAMPLER == 2) done = naive_hit(S, P, st, T.h, aov, cnt.shades);
             else done = path_hit(S, P, st, T.h, aov, cnt.shades);
+#endif
             if (done) {
                 // trace_sample epilogue (src/trace.jl:625-648)
                 cnt.paths++;
@@ -799,10 +838,11 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
                 // no bounce-0 surface was accepted: st.d is still the camera ray direction
                 if (!hit) aov_update(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
-                float4 img = A.image[pixel];
-                A.image[pixel] = make_float4(img.x * omw + target.x * w, img.y * omw + target.y * w,
-                                             img.z * omw + target.z * w, img.w * omw + target.w * w);
-                if (hit || env) A.hits[pixel] += 1;
+                acc[0] = acc[0] * omw + target.x * w;
+                acc[BLOCK] = acc[BLOCK] * omw + target.y * w;
+                acc[2 * BLOCK] = acc[2 * BLOCK] * omw + target.z * w;
+                acc[3 * BLOCK] = acc[3 * BLOCK] * omw + target.w * w;
+                if (hit || env) reinterpret_cast<int*>(acc)[10 * BLOCK] += 1;
                 if (++sample >= s_end) {
                     alive = false;
                 } else {
@@ -810,6 +850,10 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                     start_path(P, i, j, pixel, sample, st);
                 }
             }
+#if JT_STAMPS
+            unsigned long long s3 = __builtin_amdgcn_s_memtime();
+            t_fin += s3 - s2;
+#endif
             if (alive) {
                 if (SAMPLER == 1 && st.phase == PH_LIGHT) {
                     cnt.light_queries++;
@@ -819,6 +863,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                     query_begin(T, st.o, st.d, T_TLAS << 30, stack);
                 }
             }
+#if JT_STAMPS
+            t_qb += __builtin_amdgcn_s_memtime() - s3;
+#endif
         }
 #if JT_STAMPS
         t_shade += __builtin_amdgcn_s_memtime() - t1;
@@ -836,8 +883,21 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         atomicAdd(dbg + 5, lanes_n);
         atomicAdd(dbg + 6, steps_p);
         atomicAdd(dbg + 7, steps_n);
+        atomicAdd(dbg + 8, t_lhit);
+        atomicAdd(dbg + 9, t_phit);
+        atomicAdd(dbg + 10, t_fin);
+        atomicAdd(dbg + 11, t_qb);
+        atomicAdd(dbg + 12, n_lhit);
+        atomicAdd(dbg + 13, n_phit);
+        atomicAdd(dbg + 14, n_fin);
     }
 #endif
+    if (in_image) {
+        A.image[pixel] = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);
+        A.albedo[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
+        A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
+        A.hits[pixel] += reinterpret_cast<const int*>(acc)[10 * BLOCK];
+    }
     // one atomic per counter per wave
     unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
                      COUNT ? cnt.shades : 0u};
@@ -1351,16 +1411,20 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         S.o_materials = add(mats.data(), mats.size() * sizeof(DMaterial));
         S.o_lights = add(dl.data(), dl.size() * sizeof(DLight));
         S.o_cdf = add(cdf.data(), cdf.size() * sizeof(float));
-        // budget: the blob plus the stack of the chosen STACK size must leave room for >= 2
-        // workgroups per CU (160 KiB LDS); override with JT_LDS_SCENE=0 (off) or a byte budget
+        // LDS mode only when the blob does not cost workgroups per CU: the kernel holds at most
+        // 4 workgroups per CU (4 waves/SIMD), so the blob + stack + accumulators may use up to
+        // 160 KiB / 4, or as much as HBM mode's stack + accumulators already cost. Override
+        // with JT_LDS_SCENE=0 (off) or a byte budget for the blob.
         size_t budget = 48 * 1024;
         if (const char* v = std::getenv("JT_LDS_SCENE")) budget = (size_t)std::atoll(v);
         const int stack_entries = c->stack <= 16 ? 16 : c->stack <= 32 ? 32 : c->stack <= 64 ? 64 : 128;
-        const size_t stack_bytes = (size_t)stack_entries * 256 * 4;
+        const size_t base_bytes = (size_t)stack_entries * 256 * 4 + (size_t)ACC_SLOTS * BLOCK * 4;
         const size_t bytes = blob.size() * 16;
+        const size_t lds_cu = 160 * 1024;
+        const size_t wg_hbm = std::min<size_t>(4, lds_cu / base_bytes), wg_lds = lds_cu / (base_bytes + bytes);
         S.blob = nullptr;
         S.blob_n16 = 0;
-        if (bytes <= budget && bytes + stack_bytes <= 80 * 1024) {
+        if (bytes <= budget && wg_lds >= wg_hbm) {
             std::vector<uint4> b(blob);
             if ((st = upload(c, b, &S.blob))) return bail(st);
             S.blob_n16 = (int)blob.size();
@@ -1388,7 +1452,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.first = 0;
     P.seed = params->seed;
     // lanes that must be waiting before a shading phase runs; tunable
-    P.wait_lanes = 48;
+    P.wait_lanes = 40;
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
 
     // accumulators (make_trace_state: zeroed) + counters
@@ -1402,7 +1466,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     c->allocations.push_back(nrmb);
     if ((e = hipMalloc(&hits, np * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc accumulators"));
     c->allocations.push_back(hits);
-    if ((e = hipMalloc(&cnt, 16 * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc counters"));
+    if ((e = hipMalloc(&cnt, 32 * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc counters"));
     c->allocations.push_back(cnt);
     c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt};
     st = jt_reset(c);
@@ -1420,7 +1484,7 @@ int jt_reset(jt_ctx* c) {
         (e = hipMemsetAsync(c->A.albedo, 0, np * 16, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->A.normal, 0, np * 16, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->A.hits, 0, np * 8, c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->A.counters, 0, 128, c->stream)) != hipSuccess)
+        (e = hipMemsetAsync(c->A.counters, 0, 256, c->stream)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync");
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     c->first = -1;
@@ -1544,10 +1608,10 @@ int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
     return JT_OK;
 }
 
-// diagnostic build only (JT_STAMPS=1): per-phase wave clocks, read by scripts/stamps.py
+// diagnostic build only (JT_STAMPS=1): per-phase wave clocks (16 u64), read by scripts/stamps.py
 extern "C" int jt_debug_stamps(jt_ctx* c, unsigned long long* out8) {
     if (!c || !out8) return jt::fail(JT_ERR_INVALID, "NULL argument");
-    hipError_t e = hipMemcpy(out8, c->A.counters + 8, 8 * 8, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpy(out8, c->A.counters + 8, 16 * 8, hipMemcpyDeviceToHost);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy stamps");
 }
 

@@ -16,17 +16,21 @@ lib = abi.load_library()
 lib.jt_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
 scene = sceneio.load_scene(str(ROOT / "assets/scenes/cornellbox/cornellbox.json"))
 sa = abi.SceneABI(scene)
-jp = abi.make_params(Params(scene="", samples=spp, width=1280, height=720, batch=spp), 0)
+sampler = 2 if len(sys.argv) > 2 and sys.argv[2] == "naive" else 1
+jp = abi.make_params(Params(scene="", samples=spp, width=1280, height=720, batch=spp, sampler=sampler), 0)
 st = trace.make_trace_state(sa, trace.make_scene_bvh(sa, False, lib), trace.make_trace_lights(sa, lib), jp, lib)
 st.set_counters(0)
 st.trace_range(0, spp)
-v = (C.c_ulonglong * 8)()
+v = (C.c_ulonglong * 16)()
 abi.check(lib, lib.jt_debug_stamps(st.handle, v))
-t_trav, t_shade, n_trav, n_shade, lanes_p, lanes_n, steps_p, steps_n = list(v)
+t_trav, t_shade, n_trav, n_shade, lanes_p, lanes_n, steps_p, steps_n, t_lhit, t_phit, t_fin, t_qb, n_lhit, n_phit, n_fin, _ = list(v)
 tot = t_trav + t_shade
-print(f"wait_lanes={os.environ.get('JT_WAIT_LANES', 32)} spp={spp} kernel_ms={st.counters()['kernel_ms']:.1f}")
+print(f"wait_lanes={os.environ.get('JT_WAIT_LANES', 'default')} spp={spp} kernel_ms={st.counters()['kernel_ms']:.1f}")
 print(f"traversal phase {t_trav / tot:.1%}  shading phase {t_shade / tot:.1%}")
 print(f"trav iterations/wave-shade-phase {n_trav / max(1, n_shade):.2f}; cycles per trav iter {t_trav / max(1, n_trav):.0f}; "
       f"cycles per shading phase {t_shade / max(1, n_shade):.0f}")
 print(f"prim steps {steps_p} (avg lanes {lanes_p / max(1, steps_p):.1f}), node steps {steps_n} "
       f"(avg lanes {lanes_n / max(1, steps_n):.1f})")
+print(f"shading split: light_hit {t_lhit / t_shade:.1%} ({t_lhit / max(1, n_lhit):.0f} cyc x {n_lhit}), "
+      f"path_hit {t_phit / t_shade:.1%} ({t_phit / max(1, n_phit):.0f} cyc x {n_phit}), "
+      f"finish+restart {t_fin / t_shade:.1%} (phases with a finished sample {n_fin}), query_begin {t_qb / t_shade:.1%}")
