@@ -1,9 +1,9 @@
 """Generates tests/golden/scene_pins.npz from the reference's own renders
-/root/reference/images/<scene>_<sampler>.png (1280x533, RGBA8 sRGB, spp unrecorded) for the
-scenes shipped under assets/scenes (features1, features2, materials1, materials2, materials4,
-shapes1; both samplers).
+/root/reference/images/<scene>_<sampler>.png (RGBA8 sRGB, spp unrecorded) for the scenes
+shipped under assets/scenes (features1, features2, materials1, materials2, materials4, shapes1
+at 1280x533, bathroom1 at 1280x720, ecosys at 1280x640; both samplers).
 
-The fixture is data only: per block (41 rows x 40 columns, 13x32 blocks) the mean of the
+The fixture is data only: per block (41 or 40 rows x 40 columns) the mean of the
 sRGB-decoded linear values per channel, the block alpha mean and the whole-image channel mean.
 It is the statistical pin of the HIP path on these scenes (tests/test_gpu_scenes.py).
 Run in the build container (the reference is not on the GPU box):
@@ -14,9 +14,9 @@ import os
 import numpy as np
 from PIL import Image
 
-SCENES = ("features1", "features2", "materials1", "materials2", "materials4", "shapes1")
+SCENES = ("features1", "features2", "materials1", "materials2", "materials4", "shapes1", "bathroom1", "ecosys")
 OUT = os.path.join(os.path.dirname(__file__), "..", "scene_pins.npz")
-BH, BW = 41, 40
+BW = 40
 
 out = {}
 for scene in SCENES:
@@ -24,6 +24,7 @@ for scene in SCENES:
         img = np.asarray(Image.open(f"/root/reference/images/{scene}_{sampler}.png").convert("RGBA"),
                          dtype=np.uint8)
         h, w = img.shape[:2]
+        BH = 41 if h % 41 == 0 else 40
         assert h % BH == 0 and w % BW == 0, (scene, h, w)
         c = img[..., :3].astype(np.float64) / 255.0
         lin = np.where(c <= 0.04045, c / 12.92, ((c + 0.055) / 1.055) ** 2.4)
@@ -33,7 +34,7 @@ for scene in SCENES:
                                ).astype(np.float32)
         out[key + "_channel_mean"] = lin.reshape(-1, 3).mean(axis=0)
         out[key + "_size"] = np.array([w, h])
+        out[key + "_block"] = np.array([BH, BW])
         print(key, (w, h), out[key + "_channel_mean"])
-out["block"] = np.array([BH, BW])
 np.savez_compressed(OUT, **out)
 print("wrote", OUT)

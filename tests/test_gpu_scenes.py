@@ -9,6 +9,9 @@ Scene coverage of SURVEY.md §8(a):
   materials2 refractive + transparent (A28/A29)
   materials4 volumetric + refractive with a volume stack (A11/A30)
   shapes1    quads of several BLAS shapes, textured matte/glossy
+  bathroom1  config 4 (855 instances, 572 K triangles; 3 textures missing in the checkout:
+             invalid_id, i.e. constant (1,1,1,1))
+  ecosys     config 5 (12.7 K instances of 139 shapes; shape002/003 missing: dropped)
 Tolerance as tests/test_gpu_parity.py (>= 99.9 % of pixels within 1e-3 relative; image mean
 within 1e-4 relative).
 """
@@ -21,7 +24,13 @@ from conftest import ROOT, compare_images, make_params
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ("features1", "features2", "materials1", "materials2", "materials4", "shapes1")
+SCENES = ("features1", "features2", "materials1", "materials2", "materials4", "shapes1", "bathroom1", "ecosys")
+# The reference renders of these scenes hold data the checkout lacks, so the pin is loose:
+# (channel-mean rtol, block-median bound). features2: two dropped shapes; bathroom1: three
+# missing textures rendered as constant (1,1,1,1) (the renders are ~6 % brighter); ecosys:
+# two dropped shapes (the sky shows through where they stood: +20 % channel means, yet half of
+# all blocks still match to 1 %).
+INCOMPLETE = {"features2": (0.05, 0.02), "bathroom1": (0.08, 0.07), "ecosys": (0.25, 0.02)}
 _cache = {}
 
 
@@ -100,15 +109,15 @@ def test_high_quality_bvh_parity(gpu, abi, lib, oracle):
 @pytest.mark.parametrize("sampler", [1, 2])
 @pytest.mark.parametrize("name", SCENES)
 def test_statistical_pin_reference_render(gpu, abi, lib, name, sampler):
-    """HIP render at the reference's size (1280x533), 128 spp (naive: 1024), through the sRGB + 8-bit
-    pipeline, vs the reference's own PNG on 41x40-pixel block means (this also pins the HDR
-    decode, sceneio.HDR_MODE). features2's reference render holds two shapes the checkout
-    lacks (hairball, displacedsubdiv): looser channel-mean and median bounds, no p95 bound."""
+    """HIP render at the reference's size, 128 spp (naive: 1024), through the sRGB + 8-bit
+    pipeline, vs the reference's own PNG on 41x40 / 40x40-pixel block means (this also pins the
+    HDR decode, sceneio.HDR_MODE). The reference renders of INCOMPLETE scenes hold shapes or
+    textures the checkout lacks: looser channel-mean and median bounds, no p95 bound."""
     from jtrace import sceneio
     pins = np.load(Path(__file__).parent / "golden" / "scene_pins.npz")
     key = f"{name}_{'path' if sampler == 1 else 'naive'}"
     w, h = (int(v) for v in pins[key + "_size"])
-    bh, bw = (int(v) for v in pins["block"])
+    bh, bw = (int(v) for v in pins[key + "_block"])
     sa = scene_abi(name)
     spp = 128 if sampler == 1 else 1024  # the naive sampler is far noisier; the 8-bit sRGB
     p = make_params(abi, resolution=1280, samples=spp, sampler=sampler, batch=spp)  # mean is
@@ -121,8 +130,8 @@ def test_statistical_pin_reference_render(gpu, abi, lib, name, sampler):
     rel = np.abs(bm - ref) / np.maximum(ref, 0.02)
     print(key, "channel mean", cm, "reference", pins[key + "_channel_mean"],
           "block rel median", np.median(rel), "p95", np.percentile(rel, 95))
-    f2 = name == "features2"
-    np.testing.assert_allclose(cm, pins[key + "_channel_mean"], rtol=0.05 if f2 else 0.01)
-    assert np.median(rel) < (0.02 if f2 else 0.01)
-    if not f2:
+    rtol, med = INCOMPLETE.get(name, (0.01, 0.01))
+    np.testing.assert_allclose(cm, pins[key + "_channel_mean"], rtol=rtol)
+    assert np.median(rel) < med
+    if name not in INCOMPLETE:
         assert np.percentile(rel, 95) < 0.04
