@@ -91,6 +91,10 @@ struct DScene {
     // units; -1 = not in the blob). Texels, environments and LUTs stay in HBM.
     const uint4* blob;
     int blob_n16;
+    // traversal-stack overflow (scenes deeper than the LDS ring): ovf_stride entries per pixel
+    int* ovf;
+    int ovf_stride;
+    int ring;  // entries of the LDS ring in use (a power of two <= the kernel's RING)
     int o_tlas_nodes, o_tlas_prims, o_blas_nodes, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
     int o_pos, o_nrm, o_tc, o_col, o_elems, o_materials, o_lights, o_cdf;
 };

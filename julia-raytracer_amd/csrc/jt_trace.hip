@@ -237,6 +237,8 @@ __device__ __forceinline__ v3 eval_environment(const DScene& S, v3 direction) {
 // ============================================================================ traversal (src/bvh.jl)
 // Unified per-lane stack in LDS, entry = type << 30 | index. Layout stack[k * BLOCK + lane]:
 // every lane owns one bank (conflict-free ds_read/write_b32 whatever the per-lane depth).
+// The LDS part is a ring of RING entries; when a scene's bound exceeds it (OVF), the oldest
+// entries spill to a per-pixel HBM area and come back one at a time when popped.
 constexpr int BLOCK = 256;
 constexpr unsigned T_TLAS = 0u, T_INST = 1u, T_BLAS = 2u;
 constexpr unsigned IDX_MASK = (1u << 30) - 1;
@@ -262,7 +264,8 @@ struct Trav {
     v3 lo, ld, ldinv;  // the ray every node test uses: the world ray, or inside a BLAS the ray
                        // in the current instance's space (transform_ray, src/geometry.jl:107)
     float tmax;
-    int sp;            // LDS stack entries
+    int sp;            // stack entries (all levels)
+    int low;           // OVF: entries [low, sp) are in the LDS ring, [0, low) in HBM
     int inst_space;    // lo/ld/ldinv hold an instance-space ray (restore before a TLAS pop)
     int negmask;       // bit a set <=> ld[a] < 0 (the push order of src/bvh.jl:331-341, 424-434)
     int cur_inst, cur_kind;
@@ -299,6 +302,7 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     T.negmask = neg_mask(d);
     stack[0] = (int)root;
     T.sp = 1;
+    T.low = 0;
 }
 
 // One primitive of the current BLAS leaf (src/bvh.jl:444-484).
@@ -326,11 +330,36 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     T.nprim -= 1;
 }
 
-// Pop one stack entry: an instance entry or a TLAS/BLAS node.
-template <int COUNT>
-__device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, Counters& cnt) {
+template <int RING, bool OVF>
+__device__ __forceinline__ void st_push(const DScene& S, Trav& T, int* stack, int pixel, unsigned e) {
+    if (OVF) {
+        if (T.sp - T.low == S.ring) {  // ring full: the oldest entry moves to HBM
+            S.ovf[(size_t)pixel * S.ovf_stride + T.low] = stack[(T.low & (S.ring - 1)) * BLOCK];
+            T.low += 1;
+        }
+        stack[(T.sp & (S.ring - 1)) * BLOCK] = (int)e;
+    } else {
+        stack[T.sp * BLOCK] = (int)e;
+    }
+    T.sp += 1;
+}
+template <int RING, bool OVF>
+__device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* stack, int pixel) {
     T.sp -= 1;
-    const unsigned e = (unsigned)stack[T.sp * BLOCK];
+    if (OVF) {
+        if (T.sp < T.low) {  // below the ring: this entry was spilled
+            T.low = T.sp;
+            return (unsigned)S.ovf[(size_t)pixel * S.ovf_stride + T.sp];
+        }
+        return (unsigned)stack[(T.sp & (S.ring - 1)) * BLOCK];
+    }
+    return (unsigned)stack[T.sp * BLOCK];
+}
+
+// Pop one stack entry: an instance entry or a TLAS/BLAS node.
+template <int RING, bool OVF, int COUNT>
+__device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
+    const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
     const unsigned type = e >> 30, idx = e & IDX_MASK;
     if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
         if (COUNT) cnt.instances++;
@@ -349,8 +378,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         }
         T.cur_inst = (int)idx;
         T.cur_kind = ib.y;
-        stack[T.sp * BLOCK] = (int)((T_BLAS << 30) | (unsigned)ib.x);
-        T.sp += 1;
+        st_push<RING, OVF>(S, T, stack, pixel, (T_BLAS << 30) | (unsigned)ib.x);
         return;
     }
     const bool blas = type == T_BLAS;
@@ -365,14 +393,11 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         const int axis = (int)((meta >> 16) & 0xffu);
         const bool neg = (T.negmask >> axis) & 1;  // d[axis] < 0
         const unsigned tag = type << 30;
-        stack[T.sp * BLOCK] = (int)(tag | (unsigned)(neg ? start + 1 : start));
-        stack[(T.sp + 1) * BLOCK] = (int)(tag | (unsigned)(neg ? start : start + 1));
-        T.sp += 2;
+        st_push<RING, OVF>(S, T, stack, pixel, tag | (unsigned)(neg ? start + 1 : start));
+        st_push<RING, OVF>(S, T, stack, pixel, tag | (unsigned)(neg ? start : start + 1));
     } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
-        for (int k = num - 1; k >= 0; k--) {
-            stack[T.sp * BLOCK] = (int)((T_INST << 30) | (unsigned)S.tlas_prims[start + k]);
-            T.sp += 1;
-        }
+        for (int k = num - 1; k >= 0; k--)
+            st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | (unsigned)S.tlas_prims[start + k]);
     } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
@@ -731,7 +756,7 @@ struct DAccum {
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
 // mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
-template <int SAMPLER, int STACK, int COUNT>
+template <int SAMPLER, int RING, bool OVF, int COUNT>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
                                            int* stack) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -795,7 +820,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (np >= nn) {
                 if (wantp) prim_step<COUNT>(S, T, cnt);
             } else {
-                if (wantn) node_step<COUNT>(S, T, stack, cnt);
+                if (wantn) node_step<RING, OVF, COUNT>(S, T, stack, pixel, cnt);
             }
         }
 #if JT_STAMPS
@@ -919,19 +944,19 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
 
 // HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS.
-template <int SAMPLER, int STACK, int COUNT>
+template <int SAMPLER, int RING, bool OVF, int COUNT>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
-    __shared__ int lds_stack[STACK * BLOCK];
-    trace_body<SAMPLER, STACK, COUNT>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
+    __shared__ int lds_stack[RING * BLOCK];
+    trace_body<SAMPLER, RING, OVF, COUNT>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
 }
 
 // LDS mode (small scenes): the workgroup stages the scene blob into LDS once; every node,
 // instance, primitive and shading record is then a ds_read instead of a vector-memory load
 // through the TA/TD path (the measured limiter of the HBM-mode kernel).
-template <int SAMPLER, int STACK, int COUNT>
+template <int SAMPLER, int RING, bool OVF, int COUNT>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     extern __shared__ uint4 dyn_lds[];
-    uint4* blob = dyn_lds + (STACK * BLOCK) / 4;
+    uint4* blob = dyn_lds + (RING * BLOCK) / 4;
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
     DScene L = S;
@@ -951,34 +976,36 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene
     L.materials = reinterpret_cast<const DMaterial*>(blob + S.o_materials);
     L.lights = reinterpret_cast<const DLight*>(blob + S.o_lights);
     L.cdf = reinterpret_cast<const float*>(blob + S.o_cdf);
-    trace_body<SAMPLER, STACK, COUNT>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+    trace_body<SAMPLER, RING, OVF, COUNT>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
 }
 
-template <int SAMPLER, int STACK, int COUNT>
+template <int SAMPLER, int RING, bool OVF, int COUNT>
 hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st) {
     dim3 grid((P.width + 15) / 16, (P.height + 15) / 16);
     if (S.blob_n16 > 0) {
-        const size_t lds = (size_t)STACK * BLOCK * 4 + (size_t)S.blob_n16 * 16;
-        hipError_t e = hipFuncSetAttribute((const void*)trace_kernel_lds<SAMPLER, STACK, COUNT>,
+        const size_t lds = (size_t)RING * BLOCK * 4 + (size_t)S.blob_n16 * 16;
+        hipError_t e = hipFuncSetAttribute((const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, STACK, COUNT>), grid, dim3(BLOCK), lds, st, S, P, s0, s1, A);
+        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT>), grid, dim3(BLOCK), lds, st, S, P, s0, s1, A);
     } else {
-        hipLaunchKernelGGL((trace_kernel<SAMPLER, STACK, COUNT>), grid, dim3(BLOCK), 0, st, S, P, s0, s1, A);
+        hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT>), grid, dim3(BLOCK), 0, st, S, P, s0, s1, A);
     }
     return hipGetLastError();
 }
 
+// stack configurations: the whole bound in a 16-entry LDS ring, or a RING-entry ring + HBM
 template <int SAMPLER, int COUNT>
-hipError_t launch_s(int stack, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st) {
+hipError_t launch_s(int need, int ring, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A,
+                    hipStream_t st) {
 #if JT_ONE_VARIANT  // compile-time experiments only (make quick-usage): one kernel instance
-    (void)stack;
-    return launch_t<1, 16, 0>(S, P, s0, s1, A, st);
+    (void)need;
+    (void)ring;
+    return launch_t<1, 16, false, 0>(S, P, s0, s1, A, st);
 #else
-    if (stack <= 16) return launch_t<SAMPLER, 16, COUNT>(S, P, s0, s1, A, st);
-    if (stack <= 32) return launch_t<SAMPLER, 32, COUNT>(S, P, s0, s1, A, st);
-    if (stack <= 64) return launch_t<SAMPLER, 64, COUNT>(S, P, s0, s1, A, st);
-    return launch_t<SAMPLER, 128, COUNT>(S, P, s0, s1, A, st);
+    if (need <= 16) return launch_t<SAMPLER, 16, false, COUNT>(S, P, s0, s1, A, st);
+    if (ring <= 16) return launch_t<SAMPLER, 16, true, COUNT>(S, P, s0, s1, A, st);
+    return launch_t<SAMPLER, 32, true, COUNT>(S, P, s0, s1, A, st);
 #endif
 }
 
@@ -994,7 +1021,9 @@ struct jt_ctx {
     DAccum A{};
     std::vector<void*> allocations;
     int width = 0, height = 0;
-    int total_samples = 0, batch = 1, sampler = 1, stack = 16;
+    int total_samples = 0, batch = 1, sampler = 1;
+    int stack = 16;  // stack bound of the scene (entries); > 16: LDS ring of `ring` + HBM overflow
+    int ring = 16;
     int first = -1, next = 0;  // running-mean origin and next expected sample
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     size_t lds_scene_bytes = 0;  // > 0: small-scene LDS mode
@@ -1182,7 +1211,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     if (std::max(tlas_depth, max_blas_depth) + 1 > params->bvhstacksize)
         return jt::fail(JT_ERR_STACK, "BVH deeper than --bvhstacksize (the reference throws BoundsError)");
     const int need = tlas_depth + max_blas_depth + 6;  // unified stack bound
-    if (need > 128) return jt::fail(JT_ERR_UNSUPPORTED, "BVH too deep for the 128-entry LDS stack");
 
     int32_t W = 0, H = 0;
     st = jt_image_size(scene, params, &W, &H);
@@ -1198,6 +1226,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     c->batch = params->batch;
     c->sampler = params->sampler;
     c->stack = need;
+    if (const char* r = std::getenv("JT_LDS_STACK")) c->ring = std::atoi(r) > 16 ? 32 : 16;
     auto bail = [&](int status) {
         jt_destroy(c);
         return status;
@@ -1417,7 +1446,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         // with JT_LDS_SCENE=0 (off) or a byte budget for the blob.
         size_t budget = 48 * 1024;
         if (const char* v = std::getenv("JT_LDS_SCENE")) budget = (size_t)std::atoll(v);
-        const int stack_entries = c->stack <= 16 ? 16 : c->stack <= 32 ? 32 : c->stack <= 64 ? 64 : 128;
+        const int stack_entries = c->stack <= 16 ? 16 : c->ring;
         const size_t base_bytes = (size_t)stack_entries * 256 * 4 + (size_t)ACC_SLOTS * BLOCK * 4;
         const size_t bytes = blob.size() * 16;
         const size_t lds_cu = 160 * 1024;
@@ -1430,6 +1459,26 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             S.blob_n16 = (int)blob.size();
         }
         c->lds_scene_bytes = S.blob_n16 ? bytes : 0;
+    }
+    S.ovf = nullptr;
+    S.ovf_stride = 0;
+    S.ring = c->ring;
+    // JT_LDS_RING (tests only): use fewer ring entries than allocated, to exercise the overflow
+    if (const char* r = std::getenv("JT_LDS_RING")) {
+        int v = std::atoi(r);
+        if (v >= 1 && v <= 16 && (v & (v - 1)) == 0) {
+            S.ring = v;
+            c->stack = std::max(c->stack, 17);  // force the overflow-capable kernel
+            c->ring = 16;
+        }
+    }
+    if (c->stack > 16) {  // HBM overflow of the LDS stack ring: `need` entries per pixel
+        void* p = nullptr;
+        const size_t bytes = (size_t)W * (size_t)H * (size_t)need * 4;
+        if ((e = hipMalloc(&p, bytes)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc stack overflow"));
+        c->allocations.push_back(p);
+        S.ovf = (int*)p;
+        S.ovf_stride = need;
     }
 
     DParams& P = c->P;
@@ -1506,11 +1555,11 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     hipError_t e = hipEventRecord(c->ev0, c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
     if (c->sampler == JT_SAMPLER_NAIVE)
-        e = c->count ? launch_s<2, 1>(c->stack, c->S, c->P, s0, s1, c->A, c->stream)
-                     : launch_s<2, 0>(c->stack, c->S, c->P, s0, s1, c->A, c->stream);
+        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream)
+                     : launch_s<2, 0>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream);
     else
-        e = c->count ? launch_s<1, 1>(c->stack, c->S, c->P, s0, s1, c->A, c->stream)
-                     : launch_s<1, 0>(c->stack, c->S, c->P, s0, s1, c->A, c->stream);
+        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream)
+                     : launch_s<1, 0>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipEventSynchronize(c->ev1)) != hipSuccess) return hip_fail(e, "trace kernel");
@@ -1617,13 +1666,15 @@ extern "C" int jt_debug_stamps(jt_ctx* c, unsigned long long* out8) {
 
 int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     if (!c || !buf || n <= 0) return jt::fail(JT_ERR_INVALID, "NULL argument");
-    const int stack = c->stack <= 16 ? 16 : c->stack <= 32 ? 32 : c->stack <= 64 ? 64 : 128;
+    const bool ovf = c->stack > 16;
+    const int ring = ovf ? c->ring : 16;
     char tmp[512];
     std::snprintf(tmp, sizeof tmp,
-                  "kernel=%s<%d,%d,%d> mode=%s scene_lds_bytes=%zu stack=%d wait_lanes=%d grid=%dx%d block=%d",
+                  "kernel=%s<%d,%d,%s,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
+                  "wait_lanes=%d grid=%dx%d block=%d",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
-                  stack, c->count, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes, stack, c->P.wait_lanes,
-                  (c->width + 15) / 16, (c->height + 15) / 16, BLOCK);
+                  ring, ovf ? "true" : "false", c->count, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
+                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, (c->width + 15) / 16, (c->height + 15) / 16, BLOCK);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;
 }

@@ -20,7 +20,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from conftest import ROOT, compare_images, make_params
+from conftest import CORNELL, ROOT, compare_images, make_params
 
 pytestmark = pytest.mark.gpu
 
@@ -135,3 +135,31 @@ def test_statistical_pin_reference_render(gpu, abi, lib, name, sampler):
     assert np.median(rel) < med
     if name not in INCOMPLETE:
         assert np.percentile(rel, 95) < 0.04
+
+
+@pytest.mark.parametrize("name,ring", [("cornellbox", 1), ("shapes1", 2), ("bathroom1", 4)])
+def test_stack_overflow_to_hbm_is_exact(gpu, abi, lib, monkeypatch, name, ring):
+    """The LDS stack ring spills its oldest entries to HBM and reloads them when popped: with a
+    deliberately tiny ring (JT_LDS_RING, test-only) every deep traversal overflows, and the
+    image, AOVs and traversal counters must not change at all."""
+    from jtrace import sceneio, trace
+    sa = abi.SceneABI(sceneio.load_scene(CORNELL)) if name == "cornellbox" else scene_abi(name)
+    p = make_params(abi, resolution=96, samples=3)
+    bvh = trace.make_scene_bvh(sa, False, lib)
+    lights = trace.make_trace_lights(sa, lib)
+    outs = []
+    for env in (None, str(ring)):
+        if env is None:
+            monkeypatch.delenv("JT_LDS_RING", raising=False)
+        else:
+            monkeypatch.setenv("JT_LDS_RING", env)
+        st = trace.make_trace_state(sa, bvh, lights, p, lib)
+        st.trace_range(0, 3)
+        outs.append((st.get_image(), st.get_aovs(), st.counters(), st.describe()))
+        st.close()
+    assert "hbm_overflow=1" in outs[1][3], outs[1][3]
+    assert np.array_equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert np.array_equal(a, b)
+    for k in ("rays", "light_queries", "nodes", "instances", "prims", "shades"):
+        assert outs[0][2][k] == outs[1][2][k], k
