@@ -32,7 +32,8 @@ struct alignas(16) DInstTrav {
 // Shading record of an instance, 64 B: frame (12 floats) + material / shape ids.
 struct alignas(16) DInstShade {
     float4 f0, f1, f2;
-    int material, shape, mat_type, pad;
+    int material, shape, mat_type;
+    int rot_identity;  // frame x, y, z are exactly the unit axes: element normals from enrm_id
 };
 enum { KIND_TRI = 0, KIND_QUAD = 1 };
 struct alignas(16) DShape {
@@ -76,6 +77,11 @@ struct DScene {
     const float2* tc;
     const float4* col;
     const int4* elems;  // triangle (a,b,c,0) / quad (a,b,c,d), global vertex ids
+    // per element, precomputed on the host with the device's float operations:
+    // triangle_normal / quad_normal in object space, and transform_normal of it by an
+    // identity-rotation frame (eval_element_normal of an instance whose frame has no rotation)
+    const float4* enrm;
+    const float4* enrm_id;
     const DMaterial* materials;
     const DTexture* textures;
     const uchar4* texb;
@@ -96,13 +102,14 @@ struct DScene {
     int ovf_stride;
     int ring;  // entries of the LDS ring in use (a power of two <= the kernel's RING)
     int o_tlas_nodes, o_tlas_prims, o_blas_nodes, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
-    int o_pos, o_nrm, o_tc, o_col, o_elems, o_materials, o_lights, o_cdf;
+    int o_pos, o_nrm, o_tc, o_col, o_elems, o_materials, o_lights, o_cdf, o_enrm, o_enrm_id;
 };
 
 struct DCamera {
     float frame[12];
     int orthographic;
     float lens, film, aspect, focus, aperture;
+    float film_x, film_y;  // the film vector of eval_camera (src/scene.jl:377-378), host-computed
 };
 
 struct DParams {

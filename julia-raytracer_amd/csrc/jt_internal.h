@@ -38,6 +38,11 @@ inline f3 cross(f3 a, f3 b) {
     return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 inline float length(f3 a) { return std::sqrt(dot(a, a)); }
+// normalize (src/math.jl:71-78) — the same float operations as the device version
+inline f3 normalize(f3 a) {
+    const float l = std::sqrt(dot(a, a));
+    return l != 0 ? a / l : a;
+}
 inline float comp(f3 v, int axis) { return axis == 0 ? v.x : (axis == 1 ? v.y : v.z); }
 
 // Frame3f: columns x, y, z, o (src/math.jl:46)
@@ -55,6 +60,8 @@ inline void store_frame(const frame3& f, float* a) {
 }
 // transform_point (src/math.jl:80-81)
 inline f3 transform_point(const frame3& f, f3 p) { return ((f.x * p.x + f.y * p.y) + f.z * p.z) + f.o; }
+// transform_vector (src/math.jl:83-84)
+inline f3 transform_vector(const frame3& f, f3 b) { return (f.x * b.x + f.y * b.y) + f.z * b.z; }
 // inverse(frame, non_rigid) (src/math.jl:95-117)
 frame3 inverse_frame(const frame3& f, bool non_rigid);
 

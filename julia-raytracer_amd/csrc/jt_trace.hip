@@ -51,15 +51,16 @@ __device__ __forceinline__ v3 eval_position(const DScene& S, int inst, int elem,
     if (sh.kind == KIND_TRI) return transform_point(f, interp_tri(p1, p2, p3, uv));
     return transform_point(f, interp_quad(p1, p2, p3, xyz(S.pos[e.w]), uv));
 }
-// eval_element_normal (src/scene.jl:578-612)
+// eval_element_normal (src/scene.jl:578-612): transform_normal(frame, triangle/quad normal),
+// with the element normal (and, for an unrotated frame, the whole result) precomputed
+__device__ __forceinline__ v3 element_normal(const DScene& S, const DInstShade& is, const fr3& f, int g) {
+    if (is.rot_identity) return xyz(S.enrm_id[g]);
+    return transform_normal(f, xyz(S.enrm[g]));
+}
 __device__ __forceinline__ v3 eval_element_normal(const DScene& S, int inst, int elem) {
     const DInstShade& is = S.inst_shade[inst];
     const DShape sh = S.shapes[is.shape];
-    const int4 e = S.elems[sh.idx_base + elem];
-    const fr3 f = frame_from(is.f0, is.f1, is.f2);
-    v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
-    if (sh.kind == KIND_TRI) return transform_normal(f, triangle_normal(p1, p2, p3));
-    return transform_normal(f, quad_normal(p1, p2, p3, xyz(S.pos[e.w])));
+    return element_normal(S, is, frame_from(is.f0, is.f1, is.f2), sh.idx_base + elem);
 }
 // eval_normal (src/scene.jl:525-576)
 __device__ __forceinline__ v3 eval_normal(const DScene& S, const DShape& sh, const int4& e, const fr3& f, v2 uv) {
@@ -181,8 +182,7 @@ __device__ __forceinline__ void eval_shading(const DScene& S, int inst, int elem
     if (m.normal_tex >= 0) {
         normal = eval_normalmap(S, sh, e, f, m, uv);
     } else if (sh.nrm_base < 0) {
-        normal = sh.kind == KIND_TRI ? transform_normal(f, triangle_normal(p1, p2, p3))
-                                     : transform_normal(f, quad_normal(p1, p2, p3, p4));
+        normal = element_normal(S, is, f, sh.idx_base + elem);
     } else {
         normal = eval_normal(S, sh, e, f, uv);
     }
@@ -696,7 +696,7 @@ __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Pat
 // eval_camera (src/scene.jl:372-411)
 __device__ __forceinline__ void eval_camera(const DCamera& cam, v2 image_uv, v2 lens_uv, v3& ro, v3& rd) {
     const fr3 frame = frame_from(cam.frame);
-    v2 film = cam.aspect >= 1 ? V2(cam.film, cam.film / cam.aspect) : V2(cam.film * cam.aspect, cam.film);
+    const v2 film = V2(cam.film_x, cam.film_y);
     if (!cam.orthographic) {
         v3 q = V3(film.x * (0.5f - image_uv.x), film.y * (image_uv.y - 0.5f), cam.lens);
         v3 dc = -normalize(q);
@@ -973,6 +973,8 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene
     L.tc = reinterpret_cast<const float2*>(blob + S.o_tc);
     L.col = reinterpret_cast<const float4*>(blob + S.o_col);
     L.elems = reinterpret_cast<const int4*>(blob + S.o_elems);
+    L.enrm = reinterpret_cast<const float4*>(blob + S.o_enrm);
+    L.enrm_id = reinterpret_cast<const float4*>(blob + S.o_enrm_id);
     L.materials = reinterpret_cast<const DMaterial*>(blob + S.o_materials);
     L.lights = reinterpret_cast<const DLight*>(blob + S.o_lights);
     L.cdf = reinterpret_cast<const float*>(blob + S.o_cdf);
@@ -1079,6 +1081,12 @@ inline float as_f(unsigned v) {
     float f;
     std::memcpy(&f, &v, 4);
     return f;
+}
+// the frame's x, y, z columns are bitwise the unit axes (+0 entries: a -0 could flip the sign
+// of a zero normal component in transform_normal)
+bool rot_identity(const float* fv) {
+    const float id[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    return std::memcmp(fv, id, sizeof id) == 0;
 }
 DNode pack_node(const jt_bvh_node& n, int start) {
     unsigned meta = (unsigned)(uint16_t)n.num | ((unsigned)(uint8_t)n.axis << 16) | ((unsigned)(n.internal ? 1 : 0) << 24);
@@ -1245,6 +1253,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     std::vector<float4> pos, nrm, col;
     std::vector<float2> tc;
     std::vector<int4> elems;
+    std::vector<float4> enrm, enrm_id;
     for (int s = 0; s < scene->nshapes; s++) {
         const jt_shape& sh = scene->shapes[s];
         const jt_bvh_tree& t = bvh->blas[s];
@@ -1280,6 +1289,19 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                 col.push_back(f4(sh.colors[4 * v], sh.colors[4 * v + 1], sh.colors[4 * v + 2], sh.colors[4 * v + 3]));
         }
         const int nel = d.kind == KIND_TRI ? sh.ntriangles : sh.nquads;
+        // element normals (triangle_normal / quad_normal, src/geometry.jl:260-271) and their
+        // transform_normal by an unrotated frame: host float ops identical to the device's
+        for (int k = 0; k < nel; k++) {
+            const int* v = d.kind == KIND_TRI ? &sh.triangles[3 * k] : &sh.quads[4 * k];
+            auto P3 = [&](int vi) { return jt::mk3(sh.positions[3 * vi], sh.positions[3 * vi + 1], sh.positions[3 * vi + 2]); };
+            auto tri_n = [](jt::f3 a, jt::f3 b, jt::f3 cc) { return jt::normalize(jt::cross(b - a, cc - a)); };
+            jt::f3 n = d.kind == KIND_TRI ? tri_n(P3(v[0]), P3(v[1]), P3(v[2]))
+                                          : jt::normalize(tri_n(P3(v[0]), P3(v[1]), P3(v[3])) + tri_n(P3(v[2]), P3(v[3]), P3(v[1])));
+            const jt::frame3 I{jt::mk3(1, 0, 0), jt::mk3(0, 1, 0), jt::mk3(0, 0, 1), jt::mk3(0, 0, 0)};
+            const jt::f3 ni = jt::normalize(jt::transform_vector(I, n));
+            enrm.push_back(f4(n.x, n.y, n.z, 0));
+            enrm_id.push_back(f4(ni.x, ni.y, ni.z, 0));
+        }
         for (int k = 0; k < nel; k++) {
             if (d.kind == KIND_TRI)
                 elems.push_back(make_int4(d.pos_base + sh.triangles[3 * k], d.pos_base + sh.triangles[3 * k + 1],
@@ -1331,7 +1353,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         for (int q = 0; q < 12; q++) ident = ident && iv[q] == idm[q];
         iblas[k] = make_int4(d.blas_root, d.kind, ident ? 1 : 0, in.shape);
         ishade[k] = DInstShade{f4(fv[0], fv[1], fv[2], fv[3]), f4(fv[4], fv[5], fv[6], fv[7]), f4(fv[8], fv[9], fv[10], fv[11]),
-                               in.material, in.shape, scene->materials[in.material].type, 0};
+                               in.material, in.shape, scene->materials[in.material].type,
+                               rot_identity(fv) ? 1 : 0};
     }
     std::vector<DMaterial> mats(scene->nmaterials);
     for (int k = 0; k < scene->nmaterials; k++) {
@@ -1406,6 +1429,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, itrav, &S.inst_trav)) || (st = upload(c, iblas, &S.inst_blas)) || (st = upload(c, ishade, &S.inst_shade)) ||
         (st = upload(c, shapes, &S.shapes)) || (st = upload(c, pos, &S.pos)) || (st = upload(c, nrm, &S.nrm)) ||
         (st = upload(c, tc, &S.tc)) || (st = upload(c, col, &S.col)) || (st = upload(c, elems, &S.elems)) ||
+        (st = upload(c, enrm, &S.enrm)) || (st = upload(c, enrm_id, &S.enrm_id)) ||
         (st = upload(c, mats, &S.materials)) || (st = upload(c, texs, &S.textures)) || (st = upload(c, texb, &S.texb)) ||
         (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) ||
         (st = upload(c, cdf, &S.cdf)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
@@ -1437,6 +1461,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         S.o_tc = add(tc.data(), tc.size() * sizeof(float2));
         S.o_col = add(col.data(), col.size() * sizeof(float4));
         S.o_elems = add(elems.data(), elems.size() * sizeof(int4));
+        S.o_enrm = add(enrm.data(), enrm.size() * sizeof(float4));
+        S.o_enrm_id = add(enrm_id.data(), enrm_id.size() * sizeof(float4));
         S.o_materials = add(mats.data(), mats.size() * sizeof(DMaterial));
         S.o_lights = add(dl.data(), dl.size() * sizeof(DLight));
         S.o_cdf = add(cdf.data(), cdf.size() * sizeof(float));
@@ -1488,6 +1514,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.cam.lens = cam.lens;
     P.cam.film = cam.film;
     P.cam.aspect = (params->width > 0 && params->height > 0) ? (float)W / (float)H : cam.aspect;
+    // film = aspect >= 1 ? (film, film / aspect) : (film * aspect, film) (src/scene.jl:377-378)
+    P.cam.film_x = P.cam.aspect >= 1 ? cam.film : cam.film * P.cam.aspect;
+    P.cam.film_y = P.cam.aspect >= 1 ? cam.film / P.cam.aspect : cam.film;
     P.cam.focus = cam.focus;
     P.cam.aperture = cam.aperture;
     P.width = W;
