@@ -61,6 +61,11 @@ struct alignas(16) DEnv {
 };
 struct alignas(16) DLight {
     int instance, environment, cdf_offset, ncdf;
+    // guide table of a long CDF (env lights; nguide = 0: plain binary search): thresholds
+    // guide_t[k] (float) and guide_a[k] = first 0-based index i with cdf[i] > guide_t[k]
+    int guide_offset, nguide;
+    float guide_scale;  // nguide / last(cdf): first guess of the bucket of a limit
+    int pad;
 };
 
 struct DScene {
@@ -89,6 +94,8 @@ struct DScene {
     const DEnv* envs;
     const DLight* lights;
     const float* cdf;
+    const float* guide_t;   // DLight guide tables (thresholds / first indices)
+    const int* guide_a;
     const float* srgb_lut;  // srgb_to_rgb(byte_to_float(b)), 256 entries (src/color.jl:12-23)
     const float* byte_lut;  // byte_to_float(b)
     int tlas_nnodes, nenvs, nlights, pad;
@@ -382,6 +389,28 @@ __device__ __forceinline__ int sample_discrete(const float* cdf, int n, float r)
     float last = cdf[n - 1];
     r = jl_clamp(r * last, 0.0f, last - 0.00001f);
     return jl_clampi(upper_bound(cdf, n, r), 1, n);
+}
+// upper_bound through a guide table: the same first index (cdf is nondecreasing, so the answer
+// for a limit in [t_k, t_k+1) lies in [a_k, a_k+1]); a few loads instead of log2(n) dependent ones
+__device__ __forceinline__ int upper_bound_guided(const float* cdf, int n, float limit, const float* gt, const int* ga,
+                                                  int K, float scale) {
+    int k = (int)(limit * scale);
+    k = k < 0 ? 0 : (k > K - 1 ? K - 1 : k);
+    while (k > 0 && limit < gt[k]) k--;
+    while (k < K - 1 && limit >= gt[k + 1]) k++;
+    int lo = ga[k], hi = ga[k + 1];
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cdf[mid] > limit) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo >= n ? 0 : lo + 1;
+}
+__device__ __forceinline__ int sample_discrete_guided(const float* cdf, int n, float r, const float* gt, const int* ga,
+                                                      int K, float scale) {
+    float last = cdf[n - 1];
+    r = jl_clamp(r * last, 0.0f, last - 0.00001f);
+    return jl_clampi(upper_bound_guided(cdf, n, r, gt, ga, K, scale), 1, n);
 }
 __device__ __forceinline__ float sample_discrete_pdf(const float* cdf, int idx1) {  // :39-40
     return idx1 == 1 ? cdf[0] : cdf[idx1 - 1] - cdf[idx1 - 2];

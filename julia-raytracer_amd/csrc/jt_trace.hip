@@ -411,7 +411,9 @@ __device__ __forceinline__ v3 sample_lights(const DScene& S, v3 position, float 
     const DLight l = S.lights[light_id - 1];
     const float* cdf = S.cdf + l.cdf_offset;
     if (l.instance >= 0) {
-        const int element = sample_discrete(cdf, l.ncdf, rel);
+        const int element = l.nguide ? sample_discrete_guided(cdf, l.ncdf, rel, S.guide_t + l.guide_offset,
+                                                              S.guide_a + l.guide_offset, l.nguide, l.guide_scale)
+                                     : sample_discrete(cdf, l.ncdf, rel);
         const DShape sh = S.shapes[S.inst_shade[l.instance].shape];
         v2 uv = sh.kind == KIND_TRI ? sample_triangle(ruv) : ruv;
         v3 lposition = eval_position(S, l.instance, element - 1, uv);
@@ -420,7 +422,9 @@ __device__ __forceinline__ v3 sample_lights(const DScene& S, v3 position, float 
     if (l.environment >= 0) {
         const DEnv& env = S.envs[l.environment];
         const DTexture t = S.textures[env.tex];
-        const int idx = sample_discrete(cdf, l.ncdf, rel);  // 1-based, used as-is (:990-993)
+        const int idx = l.nguide ? sample_discrete_guided(cdf, l.ncdf, rel, S.guide_t + l.guide_offset,
+                                                          S.guide_a + l.guide_offset, l.nguide, l.guide_scale)
+                                 : sample_discrete(cdf, l.ncdf, rel);  // 1-based, used as-is (:990-993)
         float u = ((float)(idx % t.width) + 0.5f) / (float)t.width;
         float v = (float)((((double)idx / (double)t.width) + 0.5) / (double)t.height);
         float su, cu, sv, cv;
@@ -1414,11 +1418,29 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         d.tex = en.emission_tex;
     }
     std::vector<DLight> dl(lights->nlights);
-    std::vector<float> cdf;
+    std::vector<float> cdf, guide_t;
+    std::vector<int> guide_a;
     for (int k = 0; k < lights->nlights; k++) {
         const jt_light& l = lights->lights[k];
-        dl[k] = DLight{l.instance, l.environment, (int)cdf.size(), l.ncdf};
+        dl[k] = DLight{l.instance, l.environment, (int)cdf.size(), l.ncdf, 0, 0, 0.0f, 0};
         cdf.insert(cdf.end(), l.cdf, l.cdf + l.ncdf);
+        const float last = l.ncdf > 0 ? l.cdf[l.ncdf - 1] : 0.0f;
+        bool monotone = true;
+        for (int i = 1; i < l.ncdf && monotone; i++) monotone = l.cdf[i] >= l.cdf[i - 1];
+        if (l.ncdf >= 1024 && monotone && last > 0 && std::isfinite(last)) {
+            // K buckets of the value range; K + 1 thresholds, the last one = last(cdf)
+            const int K = std::min(65536, l.ncdf / 16);
+            dl[k].guide_offset = (int)guide_t.size();
+            dl[k].nguide = K;
+            dl[k].guide_scale = (float)K / last;
+            for (int b = 0; b <= K; b++) {
+                const float t = b == K ? last : (float)((double)last * b / K);
+                // first index with cdf[i] > t (n if none)
+                const int a = (int)(std::upper_bound(l.cdf, l.cdf + l.ncdf, t) - l.cdf);
+                guide_t.push_back(t);
+                guide_a.push_back(a);
+            }
+        }
     }
     std::vector<float> srgb, bytes;
     build_luts(srgb, bytes);
@@ -1432,7 +1454,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, enrm, &S.enrm)) || (st = upload(c, enrm_id, &S.enrm_id)) ||
         (st = upload(c, mats, &S.materials)) || (st = upload(c, texs, &S.textures)) || (st = upload(c, texb, &S.texb)) ||
         (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) ||
-        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
+        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
         return bail(st);
     S.tlas_nnodes = bvh->tlas.nnodes;
     S.nenvs = scene->nenvironments;
