@@ -117,6 +117,7 @@ struct DCamera {
     int orthographic;
     float lens, film, aspect, focus, aperture;
     float film_x, film_y;  // the film vector of eval_camera (src/scene.jl:377-378), host-computed
+    int pinhole;           // aperture is +0: only the signs of sample_disk matter
 };
 
 struct DParams {
@@ -363,6 +364,17 @@ __device__ __forceinline__ v2 sample_disk(v2 ruv) {  // src/sampling.jl:12-16
     float s, c;
     jl_sincos(phi, &s, &c);
     return V2(c * r, s * r);
+}
+// With aperture == +0, eval_camera reads sample_disk's result only through lens_uv * 0, i.e.
+// through the signs of c * r and s * r (r >= +0): those of cos(phi) and sin(phi). The float phi
+// is compared in double against the doubles nearest pi/2, pi, 3pi/2, 2pi; no float lies
+// between any of them and the true value, and cos/sin of a float are never zero except
+// sin(+0), so the signs are exactly those of the rounded jl_sincos results.
+__device__ __forceinline__ v2 sample_disk_signs(v2 ruv) {
+    const double phi = (double)(2 * pif * ruv.x);
+    const bool cneg = phi > 1.5707963267948966 && phi < 4.7123889803846897;
+    const bool sneg = phi > 3.1415926535897931 && phi < 6.2831853071795862;
+    return V2(cneg ? -0.0f : 0.0f, sneg ? -0.0f : 0.0f);
 }
 __device__ __forceinline__ float sample_hemisphere_cos_pdf(v3 normal, v3 direction) {  // :24-27
     float cosw = dot(normal, direction);

@@ -734,7 +734,7 @@ __device__ __forceinline__ void start_path(const DParams& P, int i, int j, int p
                     width * (puv.y < 0.5f ? __builtin_sqrtf(2 * puv.y) - 1 : 1 - __builtin_sqrtf(2 - 2 * puv.y)) + offset);
         uv = V2(((float)i + fuv.x) / (float)P.width, ((float)j + fuv.y) / (float)P.height);
     }
-    eval_camera(P.cam, uv, sample_disk(luv), st.o, st.d);
+    eval_camera(P.cam, uv, P.cam.pinhole ? sample_disk_signs(luv) : sample_disk(luv), st.o, st.d);
     st.radiance = V3(0, 0, 0);
     st.weight = V3(1, 1, 1);
     st.max_roughness = 0.0f;
@@ -1541,6 +1541,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.cam.film_y = P.cam.aspect >= 1 ? cam.film / P.cam.aspect : cam.film;
     P.cam.focus = cam.focus;
     P.cam.aperture = cam.aperture;
+    P.cam.pinhole = (std::signbit(cam.aperture) == 0 && cam.aperture == 0.0f) ? 1 : 0;
     P.width = W;
     P.height = H;
     P.bounces = params->bounces;
