@@ -128,6 +128,7 @@ struct DParams {
     int envhidden, tentfilter, nocaustics;
     int first;  // running-mean origin: weight of sample s is 1/(s - first + 1)
     int wait_lanes;
+    int chunk;  // samples per work unit (a tile's chunks run in order)
     unsigned long long seed;
 };
 

@@ -754,8 +754,33 @@ struct DAccum {
     float4* albedo;
     float4* normal;
     long long* hits;
-    unsigned long long* counters;  // 7 x u64: paths rays light_queries nodes instances prims shades
+    unsigned long long* counters;  // 7 x u64: paths rays light_queries nodes instances prims shades;
+                                   // [7]: tile-order wait timeouts (must stay 0)
+    unsigned* work;                // unit counter of the launch (zeroed before each launch)
+    int* tile_done;                // per 8x8 tile: sample chunks accumulated in this launch
 };
+
+// Work units: (sample chunk c, 8x8 pixel tile t), numbered chunk-major and fetched by whole
+// waves from one atomic counter, so every wave stays busy until the launch's last units.
+// A tile's chunks run in order: a wave takes (c, t) only after (c - 1, t) has published its
+// running means (agent-scope release/acquire: the two may run on different XCDs).
+__device__ __forceinline__ void wait_tile(const DAccum& A, int t, int c) {
+    if ((threadIdx.x & 63) == 0) {
+        int n = 0;
+        while (__hip_atomic_load(A.tile_done + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c) {
+            __builtin_amdgcn_s_sleep(8);
+            if (++n > (1 << 27)) {  // never expected (units are fetched in order): flag, do not hang
+                atomicAdd(A.counters + 7, 1ull);
+                break;
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+__device__ __forceinline__ void publish_tile(const DAccum& A, int t, int c) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(A.tile_done + t, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
@@ -763,16 +788,31 @@ struct DAccum {
 template <int SAMPLER, int RING, bool OVF, int COUNT>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
                                            int* stack) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int j = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    const int pixel = j * P.width + i;
-    const bool in_image = i < P.width && j < P.height;
-    bool alive = in_image && s_begin < s_end;
-    int sample = s_begin;
     __shared__ float acc_lds[ACC_SLOTS * BLOCK];
     float* acc = acc_lds + threadIdx.x;
+#if JT_STAMPS
+    unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
+    unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
+#endif
+    const int tiles_x = (P.width + 7) / 8, tiles = tiles_x * ((P.height + 7) / 8);
+    const int nchunks = (s_end - s_begin + P.chunk - 1) / P.chunk;
+    const unsigned units = (unsigned)tiles * (unsigned)nchunks;
+    for (;;) {
+    unsigned unit = 0;
+    if (lane == 0) unit = atomicAdd(A.work, 1u);
+    unit = __builtin_amdgcn_readfirstlane(unit);
+    if (unit >= units) break;
+    const int uc = (int)(unit / (unsigned)tiles), ut = (int)(unit % (unsigned)tiles);
+    if (uc > 0) wait_tile(A, ut, uc);
+    const int i = (ut % tiles_x) * 8 + (lane & 7);
+    const int j = (ut / tiles_x) * 8 + (lane >> 3);
+    const int cs0 = s_begin + uc * P.chunk, cs1 = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
+    const int pixel = j * P.width + i;
+    const bool in_image = i < P.width && j < P.height;
+    bool alive = in_image;
+    int sample = cs0;
     if (in_image) {
         const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
         acc[0] = im.x;
@@ -797,10 +837,6 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         cnt.rays++;
         query_begin(T, st.o, st.d, T_TLAS << 30, stack);
     }
-#if JT_STAMPS
-    unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
-    unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
-#endif
     for (;;) {
 #if JT_STAMPS
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -872,7 +908,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 acc[2 * BLOCK] = acc[2 * BLOCK] * omw + target.z * w;
                 acc[3 * BLOCK] = acc[3 * BLOCK] * omw + target.w * w;
                 if (hit || env) reinterpret_cast<int*>(acc)[10 * BLOCK] += 1;
-                if (++sample >= s_end) {
+                if (++sample >= cs1) {
                     alive = false;
                 } else {
                     aov.w = 1.0f / (float)(sample - P.first + 1);
@@ -901,6 +937,14 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
         if (__ballot(alive) == 0) break;
     }
+    if (in_image) {
+        A.image[pixel] = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);
+        A.albedo[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
+        A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
+        A.hits[pixel] += reinterpret_cast<const int*>(acc)[10 * BLOCK];
+    }
+    if (uc + 1 < nchunks) publish_tile(A, ut, uc);
+    }  // units
 #if JT_STAMPS
     if (lane == 0) {
         unsigned long long* dbg = A.counters + 8;
@@ -921,12 +965,6 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         atomicAdd(dbg + 14, n_fin);
     }
 #endif
-    if (in_image) {
-        A.image[pixel] = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);
-        A.albedo[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
-        A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
-        A.hits[pixel] += reinterpret_cast<const int*>(acc)[10 * BLOCK];
-    }
     // one atomic per counter per wave
     unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
                      COUNT ? cnt.shades : 0u};
@@ -985,17 +1023,26 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene
     trace_body<SAMPLER, RING, OVF, COUNT>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
 }
 
+// Persistent launch: as many workgroups as the device holds at once (capped by the number of
+// tiles), each wave then pulls work units until the launch's units are exhausted.
 template <int SAMPLER, int RING, bool OVF, int COUNT>
-hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st) {
-    dim3 grid((P.width + 15) / 16, (P.height + 15) / 16);
+hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
+    const int tiles = ((P.width + 7) / 8) * ((P.height + 7) / 8);
+    const int want = (tiles + BLOCK / 64 - 1) / (BLOCK / 64);
+    int per_cu = 0;
+    hipError_t e;
     if (S.blob_n16 > 0) {
         const size_t lds = (size_t)RING * BLOCK * 4 + (size_t)S.blob_n16 * 16;
-        hipError_t e = hipFuncSetAttribute((const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT>), grid, dim3(BLOCK), lds, st, S, P, s0, s1, A);
+        const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT>;
+        if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+        const int nwg = std::min(want, per_cu * cus);
+        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
     } else {
-        hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT>), grid, dim3(BLOCK), 0, st, S, P, s0, s1, A);
+        const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT>;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+        const int nwg = std::min(want, per_cu * cus);
+        hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
     }
     return hipGetLastError();
 }
@@ -1003,15 +1050,15 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
 // stack configurations: the whole bound in a 16-entry LDS ring, or a RING-entry ring + HBM
 template <int SAMPLER, int COUNT>
 hipError_t launch_s(int need, int ring, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A,
-                    hipStream_t st) {
+                    hipStream_t st, int cus) {
 #if JT_ONE_VARIANT  // compile-time experiments only (make quick-usage): one kernel instance
     (void)need;
     (void)ring;
-    return launch_t<1, 16, false, 0>(S, P, s0, s1, A, st);
+    return launch_t<1, 16, false, 0>(S, P, s0, s1, A, st, cus);
 #else
-    if (need <= 16) return launch_t<SAMPLER, 16, false, COUNT>(S, P, s0, s1, A, st);
-    if (ring <= 16) return launch_t<SAMPLER, 16, true, COUNT>(S, P, s0, s1, A, st);
-    return launch_t<SAMPLER, 32, true, COUNT>(S, P, s0, s1, A, st);
+    if (need <= 16) return launch_t<SAMPLER, 16, false, COUNT>(S, P, s0, s1, A, st, cus);
+    if (ring <= 16) return launch_t<SAMPLER, 16, true, COUNT>(S, P, s0, s1, A, st, cus);
+    return launch_t<SAMPLER, 32, true, COUNT>(S, P, s0, s1, A, st, cus);
 #endif
 }
 
@@ -1028,6 +1075,8 @@ struct jt_ctx {
     std::vector<void*> allocations;
     int width = 0, height = 0;
     int total_samples = 0, batch = 1, sampler = 1;
+    int cus = 256;   // compute units of the device (persistent grid size)
+    int tiles = 0;   // 8x8 pixel tiles
     int stack = 16;  // stack bound of the scene (entries); > 16: LDS ring of `ring` + HBM overflow
     int ring = 16;
     int first = -1, next = 0;  // running-mean origin and next expected sample
@@ -1553,6 +1602,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.first = 0;
     P.seed = params->seed;
     // lanes that must be waiting before a shading phase runs; tunable
+    P.chunk = 64;
+    if (const char* ch = std::getenv("JT_CHUNK")) P.chunk = std::max(1, std::atoi(ch));
     P.wait_lanes = 40;
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
 
@@ -1569,7 +1620,15 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     c->allocations.push_back(hits);
     if ((e = hipMalloc(&cnt, 32 * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc counters"));
     c->allocations.push_back(cnt);
-    c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt};
+    // persistent scheduling: unit counter + per-tile chunk counters (zeroed before each launch)
+    c->tiles = ((W + 7) / 8) * ((H + 7) / 8);
+    void* sched = nullptr;
+    if ((e = hipMalloc(&sched, (size_t)(c->tiles + 1) * 4)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc schedule"));
+    c->allocations.push_back(sched);
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, params->device) == hipSuccess && cus > 0) c->cus = cus;
+    c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt,
+                  (unsigned*)sched, (int*)sched + 1};
     st = jt_reset(c);
     if (st != JT_OK) return bail(st);
     *out = c;
@@ -1604,14 +1663,15 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     if (c->first < 0) c->first = s0;
     c->P.first = c->first;
     (void)hipSetDevice(c->device);
-    hipError_t e = hipEventRecord(c->ev0, c->stream);
-    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    hipError_t e = hipMemsetAsync(c->A.work, 0, (size_t)(c->tiles + 1) * 4, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
+    if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if (c->sampler == JT_SAMPLER_NAIVE)
-        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream)
-                     : launch_s<2, 0>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream);
+        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<2, 0>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     else
-        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream)
-                     : launch_s<1, 0>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream);
+        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<1, 0>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipEventSynchronize(c->ev1)) != hipSuccess) return hip_fail(e, "trace kernel");
@@ -1620,6 +1680,9 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     c->kernel_ms += ms;
     c->launches++;
     c->next = s1;
+    unsigned long long timeouts = 0;
+    if ((e = hipMemcpy(&timeouts, c->A.counters + 7, 8, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+    if (timeouts) return jt::fail(JT_ERR_DEVICE, "work-unit ordering wait timed out");
     return JT_OK;
 }
 

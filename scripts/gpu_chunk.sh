@@ -1,0 +1,13 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+tag=$1
+mkdir -p gpurun_out/$tag
+scripts/gpu_step.sh 300 gpurun_out/$tag/pytest_chunk.log python -m pytest tests/test_gpu_parity.py -q -rf --timeout 200 || exit 1
+grep -q "failed" gpurun_out/$tag/pytest_chunk.log && exit 1
+scripts/gpu_step.sh 1200 gpurun_out/$tag/pytest.log python -m pytest tests -q -m gpu -rf --timeout 900 || exit 1
+for ch in 32 64 256; do
+  JT_CHUNK=$ch scripts/gpu_step.sh 300 gpurun_out/$tag/bench_cb_chunk$ch.log python bench.py --no-cpu-baseline || exit 1
+done
+scripts/gpu_step.sh 600 gpurun_out/$tag/bench_f2.log python bench.py --no-cpu-baseline --scene assets/scenes/features2/features2.json --width 1920 --height 1080 --spp 64 --steps 2 --warmup 1 || exit 1
+scripts/gpu_step.sh 600 gpurun_out/$tag/bench_b1.log python bench.py --no-cpu-baseline --scene assets/scenes/bathroom1/bathroom1.json --width 1920 --height 1080 --spp 32 --steps 2 --warmup 1 || exit 1

@@ -141,3 +141,26 @@ def test_lds_and_hbm_scene_modes_bitwise_equal(gpu, abi, lib, cornell_abi, sampl
         assert np.array_equal(a, b)
     for k in ("rays", "light_queries", "nodes", "instances", "prims", "shades"):
         assert imgs[0][2][k] == imgs[1][2][k], k
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
+def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sampler, monkeypatch):
+    """Work units = (sample chunk, 8x8 tile), fetched dynamically by waves: a tile's chunks are
+    accumulated in order (cross-XCD release/acquire), so any chunk size gives the same bits."""
+    from jtrace import trace
+    bvh = trace.make_scene_bvh(cornell_abi, False, lib)
+    lights = trace.make_trace_lights(cornell_abi, lib)
+    p = make_params(abi, resolution=72, samples=9, sampler=sampler)
+    outs = []
+    for chunk in ("1000", "1", "4"):
+        monkeypatch.setenv("JT_CHUNK", chunk)
+        st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
+        st.trace_range(0, 9)
+        outs.append((st.get_image(), st.get_aovs(), st.counters()))
+        st.close()
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0])
+        for a, b in zip(outs[0][1], o[1]):
+            assert np.array_equal(a, b)
+        for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades"):
+            assert outs[0][2][k] == o[2][k], k
