@@ -1076,6 +1076,7 @@ struct jt_ctx {
     int width = 0, height = 0;
     int total_samples = 0, batch = 1, sampler = 1;
     int cus = 256;   // compute units of the device (persistent grid size)
+    int chunk = 0;   // samples per work unit (0: chosen per launch)
     int tiles = 0;   // 8x8 pixel tiles
     int stack = 16;  // stack bound of the scene (entries); > 16: LDS ring of `ring` + HBM overflow
     int ring = 16;
@@ -1602,8 +1603,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.first = 0;
     P.seed = params->seed;
     // lanes that must be waiting before a shading phase runs; tunable
-    P.chunk = 64;
+    P.chunk = 0;  // 0: per launch, a quarter of its samples within [8, 64] (enough units per wave)
     if (const char* ch = std::getenv("JT_CHUNK")) P.chunk = std::max(1, std::atoi(ch));
+    c->chunk = P.chunk;
     P.wait_lanes = 40;
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
 
@@ -1662,6 +1664,7 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
         return jt::fail(JT_ERR_STATE, "samples must be accumulated in order (expected " + std::to_string(c->next) + ")");
     if (c->first < 0) c->first = s0;
     c->P.first = c->first;
+    c->P.chunk = c->chunk > 0 ? c->chunk : std::max(8, std::min(64, (s1 - s0) / 4));
     (void)hipSetDevice(c->device);
     hipError_t e = hipMemsetAsync(c->A.work, 0, (size_t)(c->tiles + 1) * 4, c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
@@ -1786,10 +1789,10 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     char tmp[512];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d grid=%dx%d block=%d",
+                  "wait_lanes=%d chunk=%d tiles=%d block=%d",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
-                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, (c->width + 15) / 16, (c->height + 15) / 16, BLOCK);
+                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.chunk, c->tiles, BLOCK);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;
 }
