@@ -830,7 +830,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     Aov aov{acc, 1.0f / (float)(sample - P.first + 1)};
     Path st;
     Trav T;
-    T.sp = 0;
+    // lane states, from the stack cursor alone: sp < 0 finished (no samples left), nprim > 0 or
+    // sp > 0 in a query, sp == nprim == 0 waiting for the shading phase
+    T.sp = -1;
     T.nprim = 0;
     if (alive) {
         start_path(P, i, j, pixel, sample, st);
@@ -846,11 +848,11 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         // majority (a wave-uniform branch), so the SIMD executes one code path per iteration.
         // A lane's own sequence of steps is unchanged: it only waits while the other kind runs.
         for (;;) {
-            const bool wantp = alive && T.nprim > 0;
-            const bool wantn = alive && T.nprim == 0 && T.sp > 0;
+            const bool wantp = T.nprim > 0;
+            const bool wantn = T.nprim == 0 && T.sp > 0;
             const int np = __popcll(__ballot(wantp));
             const int nn = __popcll(__ballot(wantn));
-            const int nw = __popcll(__ballot(alive && !wantp && !wantn));
+            const int nw = __popcll(__ballot((T.sp | T.nprim) == 0));
             const int nb = np + nn;
             if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
 #if JT_STAMPS
@@ -869,7 +871,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         n_shade++;
 #endif
         // shading phase: every waiting lane consumes its hit and issues its next query
-        if (alive && !query_busy(T)) {
+        if ((T.sp | T.nprim) == 0) {
+            bool alive = true;
             const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
             bool done;
 #if JT_STAMPS
@@ -910,6 +913,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 if (hit || env) reinterpret_cast<int*>(acc)[10 * BLOCK] += 1;
                 if (++sample >= cs1) {
                     alive = false;
+                    T.sp = -1;
                 } else {
                     aov.w = 1.0f / (float)(sample - P.first + 1);
                     start_path(P, i, j, pixel, sample, st);
@@ -935,7 +939,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #if JT_STAMPS
         t_shade += __builtin_amdgcn_s_memtime() - t1;
 #endif
-        if (__ballot(alive) == 0) break;
+        if (__ballot(T.sp >= 0) == 0) break;
     }
     if (in_image) {
         A.image[pixel] = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);

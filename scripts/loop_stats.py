@@ -10,9 +10,11 @@ s = open(path).read().split("\n")
 start = next(i for i, l in enumerate(s) if l.startswith(name))
 end = next(i for i in range(start, len(s)) if s[i].startswith(".Lfunc_end"))
 k = s[start:end]
-b = next(i for i, l in enumerate(k) if "s_bcnt1" in l)
-h = next(i for i in range(b, 0, -1) if "This Loop Header: Depth=2" in k[i])
-hdr = re.match(r"\.LBB\d+_\d+", k[h - 1]).group(0)
+# the traversal loop: the innermost loop around the first run of >= 3 s_bcnt1 (the step ballots)
+bc = [i for i, l in enumerate(k) if "s_bcnt1" in l]
+b = next(bc[n] for n in range(len(bc) - 2) if bc[n + 2] - bc[n] < 40)
+h = next(i for i in range(b, 0, -1) if "This Loop Header:" in k[i])
+hdr = next(re.match(r"\.LBB\d+_\d+", k[i]).group(0) for i in range(h, 0, -1) if k[i].startswith(".LBB"))
 body = [l for l in k[h - 1:] ]
 # the loop ends at the last line that is "in Loop: Header=<hdr>" region: take blocks whose
 # comment names this header (or deeper loops nested in it)
