@@ -756,14 +756,18 @@ struct DAccum {
     long long* hits;
     unsigned long long* counters;  // 7 x u64: paths rays light_queries nodes instances prims shades;
                                    // [7]: tile-order wait timeouts (must stay 0)
-    unsigned* work;                // unit counter of the launch (zeroed before each launch)
+    unsigned* work;                // unit counters of the launch, one per XCD band at work[16 b]
+                                   // (zeroed before each launch)
     int* tile_done;                // per 8x8 tile: sample chunks accumulated in this launch
 };
 
-// Work units: (sample chunk c, 8x8 pixel tile t), numbered chunk-major and fetched by whole
-// waves from one atomic counter, so every wave stays busy until the launch's last units.
-// A tile's chunks run in order: a wave takes (c, t) only after (c - 1, t) has published its
-// running means (agent-scope release/acquire: the two may run on different XCDs).
+// Work units: (sample chunk c, 8x8 pixel tile t), fetched by whole waves from atomic counters,
+// so every wave stays busy until the launch's last units. The tiles are split into 8 bands of
+// rows, one per XCD: a wave drains its own XCD's band first (neighbouring pixels share that
+// XCD's L2), then helps the other bands. Within a band units are numbered chunk-major, and a
+// tile's chunks run in order: a wave takes (c, t) only after (c - 1, t) has published its
+// running means (agent-scope release/acquire: a helper may run on another XCD).
+constexpr int NBANDS = 8, BAND_STRIDE = 16;
 __device__ __forceinline__ void wait_tile(const DAccum& A, int t, int c) {
     if ((threadIdx.x & 63) == 0) {
         int n = 0;
@@ -798,13 +802,20 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
     const int tiles_x = (P.width + 7) / 8, tiles = tiles_x * ((P.height + 7) / 8);
     const int nchunks = (s_end - s_begin + P.chunk - 1) / P.chunk;
-    const unsigned units = (unsigned)tiles * (unsigned)nchunks;
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    int band_k = 0;
     for (;;) {
+    const int band = (int)((xcc + (unsigned)band_k) & (NBANDS - 1));
+    const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
     unsigned unit = 0;
-    if (lane == 0) unit = atomicAdd(A.work, 1u);
+    if (lane == 0) unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
     unit = __builtin_amdgcn_readfirstlane(unit);
-    if (unit >= units) break;
-    const int uc = (int)(unit / (unsigned)tiles), ut = (int)(unit % (unsigned)tiles);
+    if (unit >= (unsigned)bn * (unsigned)nchunks) {  // this band is drained: help the next one
+        if (++band_k >= NBANDS) break;
+        continue;
+    }
+    const int uc = (int)(unit / (unsigned)bn), ut = bt0 + (int)(unit % (unsigned)bn);
     if (uc > 0) wait_tile(A, ut, uc);
     const int i = (ut % tiles_x) * 8 + (lane & 7);
     const int j = (ut / tiles_x) * 8 + (lane >> 3);
@@ -1629,12 +1640,13 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     // persistent scheduling: unit counter + per-tile chunk counters (zeroed before each launch)
     c->tiles = ((W + 7) / 8) * ((H + 7) / 8);
     void* sched = nullptr;
-    if ((e = hipMalloc(&sched, (size_t)(c->tiles + 1) * 4)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc schedule"));
+    if ((e = hipMalloc(&sched, (size_t)(c->tiles + NBANDS * BAND_STRIDE) * 4)) != hipSuccess)
+        return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc schedule"));
     c->allocations.push_back(sched);
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, params->device) == hipSuccess && cus > 0) c->cus = cus;
     c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt,
-                  (unsigned*)sched, (int*)sched + 1};
+                  (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE};
     st = jt_reset(c);
     if (st != JT_OK) return bail(st);
     *out = c;
@@ -1670,7 +1682,7 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     c->P.first = c->first;
     c->P.chunk = c->chunk > 0 ? c->chunk : std::max(8, std::min(64, (s1 - s0) / 4));
     (void)hipSetDevice(c->device);
-    hipError_t e = hipMemsetAsync(c->A.work, 0, (size_t)(c->tiles + 1) * 4, c->stream);
+    hipError_t e = hipMemsetAsync(c->A.work, 0, (size_t)(c->tiles + NBANDS * BAND_STRIDE) * 4, c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
     if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if (c->sampler == JT_SAMPLER_NAIVE)
