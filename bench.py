@@ -137,9 +137,12 @@ def main():
 
     def step():
         state.reset()
-        state.trace_range(s0, s1)
+        state.trace_range(s0, s1)  # returns when the launch has finished (HIP event sync)
         if world > 1:  # the path's one exchange: sum of sample-weighted shard means (RCCL)
             reduce_running_means(img_t, s1 - s0, S, dist, dst=0)
+            # the reduce reads the library's buffer on torch's stream: finish it before the next
+            # step's jt_reset clears that buffer on the library's stream
+            torch.cuda.synchronize()
         return state.counters()
 
     for _ in range(args.warmup):

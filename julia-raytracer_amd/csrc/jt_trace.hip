@@ -270,7 +270,8 @@ struct Trav {
     int negmask;       // bit a set <=> ld[a] < 0 (the push order of src/bvh.jl:331-341, 424-434)
     int cur_inst, cur_kind;
     int prim, nprim;   // leaf cursor: next primitive record, primitives left
-    Hit h;
+    int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
+    float h_u, h_v;
 };
 
 __device__ __forceinline__ int neg_mask(v3 d) { return (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0); }
@@ -283,6 +284,10 @@ __device__ __forceinline__ void world_ray(Trav& T) {
     T.inst_space = 0;
 }
 
+__device__ __forceinline__ Hit query_hit(const Trav& T) {
+    return Hit{T.h_inst, T.h_elem, T.h_u, T.h_v, T.tmax, T.h_inst >= 0};
+}
+
 __device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T.nprim > 0; }
 
 __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, int* stack) {
@@ -293,7 +298,10 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     T.ld = d;
     T.ldinv = T.wdinv;
     T.tmax = __builtin_inff();
-    T.h = Hit{-1, -1, 0, 0, 0, false};
+    T.h_inst = -1;
+    T.h_elem = -1;
+    T.h_u = 0;
+    T.h_v = 0;
     T.nprim = 0;
     T.prim = 0;
     T.cur_inst = -1;
@@ -323,7 +331,10 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
         p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
     }
     if (p.hit) {
-        T.h = Hit{T.cur_inst, elem, p.u, p.v, p.t, true};
+        T.h_inst = T.cur_inst;
+        T.h_elem = elem;
+        T.h_u = p.u;
+        T.h_v = p.v;
         T.tmax = p.t;
     }
     T.prim += 1;
@@ -888,20 +899,20 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             bool done;
 #if JT_STAMPS
             unsigned long long s0 = __builtin_amdgcn_s_memtime();
-            if (light) done = light_hit(S, P, st, T.h);
+            if (light) done = light_hit(S, P, st, query_hit(T));
             unsigned long long s1 = __builtin_amdgcn_s_memtime();
             if (!light) {
-                if (SAMPLER == 2) done = naive_hit(S, P, st, T.h, aov, cnt.shades);
-                else done = path_hit(S, P, st, T.h, aov, cnt.shades);
+                if (SAMPLER == 2) done = naive_hit(S, P, st, query_hit(T), aov, cnt.shades);
+                else done = path_hit(S, P, st, query_hit(T), aov, cnt.shades);
             }
             unsigned long long s2 = __builtin_amdgcn_s_memtime();
             if (__ballot(light)) { t_lhit += s1 - s0; n_lhit++; }
             if (__ballot(!light)) { t_phit += s2 - s1; n_phit++; }
             if (__ballot(done)) n_fin++;
 #else
-            if (light) done = light_hit(S, P, st, T.h);
-            else if (SAMPLER == 2) done = naive_hit(S, P, st, T.h, aov, cnt.shades);
-            else done = path_hit(S, P, st, T.h, aov, cnt.shades);
+            if (light) done = light_hit(S, P, st, query_hit(T));
+            else if (SAMPLER == 2) done = naive_hit(S, P, st, query_hit(T), aov, cnt.shades);
+            else done = path_hit(S, P, st, query_hit(T), aov, cnt.shades);
 #endif
             if (done) {
                 // trace_sample epilogue (src/trace.jl:625-648)
