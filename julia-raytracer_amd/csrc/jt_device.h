@@ -69,10 +69,9 @@ struct alignas(16) DLight {
 };
 
 struct DScene {
-    const DNode* tlas_nodes;
+    const DNode* nodes;      // TLAS nodes, then every BLAS (global node indices)
     const int* tlas_prims;  // instance ids in leaf order
-    const DNode* blas_nodes;
-    const float4* prims;  // triangle: 3 float4 (p1|elem, p2, p3); quad: 4 float4 (p4.w = p3==p4)
+    const float4* prims;  // triangle: 3 float4 (p1|elem, p2-p1, p3-p1); quad: 4 float4 (p4.w = p3==p4)
     const DInstTrav* inst_trav;
     const int4* inst_blas;  // per instance: blas_root, kind, identity-transform flag, shape
     const DInstShade* inst_shade;
@@ -108,7 +107,7 @@ struct DScene {
     int* ovf;
     int ovf_stride;
     int ring;  // entries of the LDS ring in use (a power of two <= the kernel's RING)
-    int o_tlas_nodes, o_tlas_prims, o_blas_nodes, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
+    int o_nodes, o_tlas_prims, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
     int o_pos, o_nrm, o_tc, o_col, o_elems, o_materials, o_lights, o_cdf, o_enrm, o_enrm_id;
 };
 
@@ -479,8 +478,7 @@ struct PrimHit {
 // intersect_triangle (src/geometry.jl:206-236), branchless: every quantity is computed and the
 // reference's early-out tests are combined into one predicate (the same comparisons, so NaN
 // behaves as in the reference: a NaN u, v or t fails none of them). A miss is (0, 0, inf).
-__device__ __forceinline__ PrimHit intersect_triangle(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 p2, v3 p3) {
-    v3 edge1 = p2 - p1, edge2 = p3 - p1;
+__device__ __forceinline__ PrimHit intersect_triangle_e(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 edge1, v3 edge2) {
     v3 pvec = cross(d, edge2);
     float det = dot(edge1, pvec);
     float inv_det = 1.0f / det;
@@ -496,6 +494,10 @@ __device__ __forceinline__ PrimHit intersect_triangle(v3 o, v3 d, float tmin, fl
     r.t = miss ? __builtin_inff() : t;
     r.hit = !miss;
     return r;
+}
+// triangle records carry the edges p2 - p1, p3 - p1, precomputed on the host (the same floats)
+__device__ __forceinline__ PrimHit intersect_triangle(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 p2, v3 p3) {
+    return intersect_triangle_e(o, d, tmin, tmax, p1, p2 - p1, p3 - p1);
 }
 // intersect_quad (src/geometry.jl:238-258); `degenerate` = (p3 == p4), precomputed on the host
 __device__ __forceinline__ PrimHit intersect_quad(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 p2, v3 p3, v3 p4,

@@ -323,7 +323,7 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
         const float4* r = S.prims + 3 * T.prim;
         const float4 a = r[0], b = r[1], c = r[2];
         elem = __float_as_int(a.w);
-        p = intersect_triangle(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c));
+        p = intersect_triangle_e(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c));  // (p1, edge1, edge2)
     } else {
         const float4* r = S.prims + 4 * T.prim;
         const float4 a = r[0], b = r[1], c = r[2], d = r[3];
@@ -394,7 +394,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
     }
     const bool blas = type == T_BLAS;
     if (!blas && T.inst_space) world_ray(T);  // back from an instance: TLAS nodes test the world ray
-    const DNode nd = blas ? S.blas_nodes[idx] : S.tlas_nodes[idx];
+    const DNode nd = S.nodes[idx];
     if (COUNT) cnt.nodes++;
     if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
     const unsigned meta = __float_as_uint(nd.b.w);
@@ -755,6 +755,11 @@ __device__ __forceinline__ void start_path(const DParams& P, int i, int j, int p
     st.phase = PH_SCENE;
 }
 
+// active lanes of a ballot, as a 32-bit scalar (keeps the comparisons of counts on the SALU)
+__device__ __forceinline__ int lane_count(unsigned long long m) {
+    return __builtin_popcount((unsigned)m) + __builtin_popcount((unsigned)(m >> 32));
+}
+
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
@@ -872,9 +877,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         for (;;) {
             const bool wantp = T.nprim > 0;
             const bool wantn = T.nprim == 0 && T.sp > 0;
-            const int np = __popcll(__ballot(wantp));
-            const int nn = __popcll(__ballot(wantn));
-            const int nw = __popcll(__ballot((T.sp | T.nprim) == 0));
+            const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
+            const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
+            const int nw = lane_count(__builtin_amdgcn_ballot_w64((T.sp | T.nprim) == 0));
             const int nb = np + nn;
             if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
 #if JT_STAMPS
@@ -882,9 +887,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (np >= nn) { steps_p++; lanes_p += np; } else { steps_n++; lanes_n += nn; }
 #endif
             if (np >= nn) {
-                if (wantp) prim_step<COUNT>(S, T, cnt);
+                if (T.nprim > 0) prim_step<COUNT>(S, T, cnt);
             } else {
-                if (wantn) node_step<RING, OVF, COUNT>(S, T, stack, pixel, cnt);
+                if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT>(S, T, stack, pixel, cnt);
             }
         }
 #if JT_STAMPS
@@ -1028,9 +1033,8 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
     DScene L = S;
-    L.tlas_nodes = reinterpret_cast<const DNode*>(blob + S.o_tlas_nodes);
+    L.nodes = reinterpret_cast<const DNode*>(blob + S.o_nodes);
     L.tlas_prims = reinterpret_cast<const int*>(blob + S.o_tlas_prims);
-    L.blas_nodes = reinterpret_cast<const DNode*>(blob + S.o_blas_nodes);
     L.prims = reinterpret_cast<const float4*>(blob + S.o_prims);
     L.inst_trav = reinterpret_cast<const DInstTrav*>(blob + S.o_inst_trav);
     L.inst_blas = reinterpret_cast<const int4*>(blob + S.o_inst_blas);
@@ -1340,7 +1344,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         DShape& d = shapes[s];
         d.kind = sh.ntriangles ? KIND_TRI : KIND_QUAD;
         const int stride = d.kind == KIND_TRI ? 3 : 4;
-        d.blas_root = (int)blas.size();
+        d.blas_root = bvh->tlas.nnodes + (int)blas.size();  // global index: TLAS nodes come first
         // records are 3 (triangle) or 4 (quad) float4s: align the shape's first record to its
         // stride so prim_base * stride addresses it exactly when shape kinds are mixed
         while (prims.size() % stride) prims.push_back(f4(0, 0, 0, 0));
@@ -1403,8 +1407,13 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             float4 a = P3(v[0]), b = P3(v[1]), cc = P3(v[2]);
             a.w = as_f(el);
             prims.push_back(a);
-            prims.push_back(b);
-            prims.push_back(cc);
+            if (d.kind == KIND_TRI) {  // edge1 = p2 - p1, edge2 = p3 - p1 (src/geometry.jl:208-209)
+                prims.push_back(f4(b.x - a.x, b.y - a.y, b.z - a.z, 0));
+                prims.push_back(f4(cc.x - a.x, cc.y - a.y, cc.z - a.z, 0));
+            } else {
+                prims.push_back(b);
+                prims.push_back(cc);
+            }
             if (d.kind == KIND_QUAD) {
                 float4 dd = P3(v[3]);
                 const bool degenerate = cc.x == dd.x && cc.y == dd.y && cc.z == dd.z;  // p3 == p4
@@ -1522,8 +1531,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     build_luts(srgb, bytes);
 
     DScene& S = c->S;
-    if ((st = upload(c, tlas, &S.tlas_nodes)) || (st = upload(c, tlas_prims, &S.tlas_prims)) ||
-        (st = upload(c, blas, &S.blas_nodes)) || (st = upload(c, prims, &S.prims)) ||
+    std::vector<DNode> nodes(tlas);
+    nodes.insert(nodes.end(), blas.begin(), blas.end());
+    if ((st = upload(c, nodes, &S.nodes)) || (st = upload(c, tlas_prims, &S.tlas_prims)) || (st = upload(c, prims, &S.prims)) ||
         (st = upload(c, itrav, &S.inst_trav)) || (st = upload(c, iblas, &S.inst_blas)) || (st = upload(c, ishade, &S.inst_shade)) ||
         (st = upload(c, shapes, &S.shapes)) || (st = upload(c, pos, &S.pos)) || (st = upload(c, nrm, &S.nrm)) ||
         (st = upload(c, tc, &S.tc)) || (st = upload(c, col, &S.col)) || (st = upload(c, elems, &S.elems)) ||
@@ -1546,9 +1556,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             if (bytes) std::memcpy(blob.data() + off, data, bytes);
             return off;
         };
-        S.o_tlas_nodes = add(tlas.data(), tlas.size() * sizeof(DNode));
+        S.o_nodes = add(nodes.data(), nodes.size() * sizeof(DNode));
         S.o_tlas_prims = add(tlas_prims.data(), tlas_prims.size() * sizeof(int));
-        S.o_blas_nodes = add(blas.data(), blas.size() * sizeof(DNode));
         S.o_prims = add(prims.data(), prims.size() * sizeof(float4));
         S.o_inst_trav = add(itrav.data(), itrav.size() * sizeof(DInstTrav));
         S.o_inst_blas = add(iblas.data(), iblas.size() * sizeof(int4));
