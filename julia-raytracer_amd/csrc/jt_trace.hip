@@ -367,11 +367,14 @@ __device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* 
     return (unsigned)stack[T.sp * BLOCK];
 }
 
-// Pop one stack entry: an instance entry or a TLAS/BLAS node.
+// Pop one stack entry: an instance entry or a TLAS/BLAS node. An instance visit and the box
+// test of its BLAS root are one step: the reference's instance visit pushes nothing but the
+// root (src/bvh.jl:345-351, 502-506), which is then the very next pop, so testing it in the same
+// step visits the same nodes in the same order.
 template <int RING, bool OVF, int COUNT>
 __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
     const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
-    const unsigned type = e >> 30, idx = e & IDX_MASK;
+    unsigned type = e >> 30, idx = e & IDX_MASK;
     if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
         if (COUNT) cnt.instances++;
         const int4 ib = S.inst_blas[idx];  // blas_root, kind, identity, shape
@@ -389,11 +392,12 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         }
         T.cur_inst = (int)idx;
         T.cur_kind = ib.y;
-        st_push<RING, OVF>(S, T, stack, pixel, (T_BLAS << 30) | (unsigned)ib.x);
-        return;
+        type = T_BLAS;
+        idx = (unsigned)ib.x;
+    } else if (type == T_TLAS && T.inst_space) {
+        world_ray(T);  // back from an instance: TLAS nodes test the world ray
     }
     const bool blas = type == T_BLAS;
-    if (!blas && T.inst_space) world_ray(T);  // back from an instance: TLAS nodes test the world ray
     const DNode nd = S.nodes[idx];
     if (COUNT) cnt.nodes++;
     if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
