@@ -42,13 +42,14 @@ __device__ __forceinline__ fr3 inst_frame(const DScene& S, int inst) {
 }
 
 // eval_position (src/scene.jl:435-476)
+template <int F>
 __device__ __forceinline__ v3 eval_position(const DScene& S, int inst, int elem, v2 uv) {
     const DInstShade& is = S.inst_shade[inst];
     const DShape sh = S.shapes[is.shape];
     const int4 e = S.elems[sh.idx_base + elem];
     const fr3 f = frame_from(is.f0, is.f1, is.f2);
     v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
-    if (sh.kind == KIND_TRI) return transform_point(f, interp_tri(p1, p2, p3, uv));
+    if (!(F & FT_QUAD) || sh.kind == KIND_TRI) return transform_point(f, interp_tri(p1, p2, p3, uv));
     return transform_point(f, interp_quad(p1, p2, p3, xyz(S.pos[e.w]), uv));
 }
 // eval_element_normal (src/scene.jl:578-612): transform_normal(frame, triangle/quad normal),
@@ -166,6 +167,7 @@ struct Shading {
 };
 
 // eval_shading_position + eval_shading_normal + eval_material (src/scene.jl:416-673)
+template <int F>
 __device__ __forceinline__ void eval_shading(const DScene& S, int inst, int elem, v2 uv, v3 outgoing, Shading& out) {
     const DInstShade is = S.inst_shade[inst];
     const DShape sh = S.shapes[is.shape];
@@ -173,30 +175,33 @@ __device__ __forceinline__ void eval_shading(const DScene& S, int inst, int elem
     const fr3 f = frame_from(is.f0, is.f1, is.f2);
     const DMaterial& m = S.materials[is.material];
     v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
-    v3 p4 = sh.kind == KIND_QUAD ? xyz(S.pos[e.w]) : p3;
+    const bool tri = !(F & FT_QUAD) || sh.kind == KIND_TRI;
+    v3 p4 = !tri ? xyz(S.pos[e.w]) : p3;
     // position
-    out.position = sh.kind == KIND_TRI ? transform_point(f, interp_tri(p1, p2, p3, uv))
-                                       : transform_point(f, interp_quad(p1, p2, p3, p4, uv));
+    out.position = tri ? transform_point(f, interp_tri(p1, p2, p3, uv))
+                       : transform_point(f, interp_quad(p1, p2, p3, p4, uv));
     // shading normal
+    const int mtype = (F & FT_MAT) ? m.type : (int)M_MATTE;
     v3 normal;
-    if (m.normal_tex >= 0) {
+    if ((F & FT_TEX) && m.normal_tex >= 0) {
         normal = eval_normalmap(S, sh, e, f, m, uv);
-    } else if (sh.nrm_base < 0) {
+    } else if (!(F & FT_ATTR) || sh.nrm_base < 0) {
         normal = element_normal(S, is, f, sh.idx_base + elem);
     } else {
         normal = eval_normal(S, sh, e, f, uv);
     }
-    if (m.type != M_REFRACTIVE) normal = dot(normal, outgoing) >= 0 ? normal : -normal;
+    if (mtype != M_REFRACTIVE) normal = dot(normal, outgoing) >= 0 ? normal : -normal;
     out.normal = normal;
     // material point
     MatPoint& p = out.mat;
-    v2 texcoord = eval_texcoord(S, sh, e, uv);
-    v4 emission_tex = eval_texture(S, m.emission_tex, texcoord, true);
-    v4 color_shp = eval_color(S, sh, e, uv);
-    v4 color_tex = eval_texture(S, m.color_tex, texcoord, true);
-    v4 roughness_tex = eval_texture(S, m.roughness_tex, texcoord, false);
-    v4 scattering_tex = eval_texture(S, m.scattering_tex, texcoord, true);
-    p.type = m.type;
+    const v4 one = V4(1, 1, 1, 1);
+    v2 texcoord = (F & FT_ATTR) ? eval_texcoord(S, sh, e, uv) : uv;
+    v4 emission_tex = (F & FT_TEX) ? eval_texture(S, m.emission_tex, texcoord, true) : one;
+    v4 color_shp = (F & FT_ATTR) ? eval_color(S, sh, e, uv) : one;
+    v4 color_tex = (F & FT_TEX) ? eval_texture(S, m.color_tex, texcoord, true) : one;
+    v4 roughness_tex = (F & FT_TEX) ? eval_texture(S, m.roughness_tex, texcoord, false) : one;
+    v4 scattering_tex = (F & FT_TEX) ? eval_texture(S, m.scattering_tex, texcoord, true) : one;
+    p.type = mtype;
     p.emission = V3(m.emission[0], m.emission[1], m.emission[2]) * xyz(emission_tex);
     p.color = (V3(m.color[0], m.color[1], m.color[2]) * xyz(color_tex)) * xyz(color_shp);
     p.opacity = m.opacity * color_tex.w * color_shp.w;
@@ -207,22 +212,24 @@ __device__ __forceinline__ void eval_shading(const DScene& S, int inst, int elem
     p.scattering = V3(m.scattering[0], m.scattering[1], m.scattering[2]) * xyz(scattering_tex);
     p.scanisotropy = m.scanisotropy;
     p.trdepth = m.trdepth;
-    if (m.type == M_REFRACTIVE || m.type == M_VOLUMETRIC || m.type == M_SUBSURFACE) {
+    if (mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE) {
         p.density = V3(-jl_log(jl_clamp(p.color.x, 0.0001f, 1.0f)) / p.trdepth,
                        -jl_log(jl_clamp(p.color.y, 0.0001f, 1.0f)) / p.trdepth,
                        -jl_log(jl_clamp(p.color.z, 0.0001f, 1.0f)) / p.trdepth);
     } else {
         p.density = V3(0, 0, 0);
     }
-    if (m.type == M_MATTE || m.type == M_GLTFPBR || m.type == M_GLOSSY) roughness = jl_clamp(roughness, min_roughness, 1.0f);
-    else if (m.type == M_VOLUMETRIC) roughness = 0.0f;
+    if (mtype == M_MATTE || mtype == M_GLTFPBR || mtype == M_GLOSSY) roughness = jl_clamp(roughness, min_roughness, 1.0f);
+    else if (mtype == M_VOLUMETRIC) roughness = 0.0f;
     else if (roughness < min_roughness) roughness = 0.0f;
     p.roughness = roughness;
 }
 
 // eval_environment (src/scene.jl:893-914)
+template <int F>
 __device__ __forceinline__ v3 eval_environment(const DScene& S, v3 direction) {
     v3 emission = V3(0, 0, 0);
+    if (!(F & FT_ENV)) return emission;  // no environments: the sum is empty
     for (int k = 0; k < S.nenvs; k++) {
         const DEnv& env = S.envs[k];
         v3 wl = transform_direction(frame_from(env.inv), direction);
@@ -314,12 +321,12 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
 }
 
 // One primitive of the current BLAS leaf (src/bvh.jl:444-484).
-template <int COUNT>
+template <int COUNT, int F>
 __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cnt) {
     if (COUNT) cnt.prims++;
     PrimHit p;
     int elem;
-    if (T.cur_kind == KIND_TRI) {
+    if (!(F & FT_QUAD) || T.cur_kind == KIND_TRI) {
         const float4* r = S.prims + 3 * T.prim;
         const float4 a = r[0], b = r[1], c = r[2];
         elem = __float_as_int(a.w);
@@ -421,6 +428,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
 
 // ============================================================================ lights (src/trace.jl)
 // sample_lights (src/trace.jl:968-1008)
+template <int F>
 __device__ __forceinline__ v3 sample_lights(const DScene& S, v3 position, float rl, float rel, v2 ruv) {
     const int light_id = sample_uniform(S.nlights, rl);
     const DLight l = S.lights[light_id - 1];
@@ -430,11 +438,11 @@ __device__ __forceinline__ v3 sample_lights(const DScene& S, v3 position, float 
                                                               S.guide_a + l.guide_offset, l.nguide, l.guide_scale)
                                      : sample_discrete(cdf, l.ncdf, rel);
         const DShape sh = S.shapes[S.inst_shade[l.instance].shape];
-        v2 uv = sh.kind == KIND_TRI ? sample_triangle(ruv) : ruv;
-        v3 lposition = eval_position(S, l.instance, element - 1, uv);
+        v2 uv = (!(F & FT_QUAD) || sh.kind == KIND_TRI) ? sample_triangle(ruv) : ruv;
+        v3 lposition = eval_position<F>(S, l.instance, element - 1, uv);
         return normalize(lposition - position);
     }
-    if (l.environment >= 0) {
+    if ((F & FT_ENV) && l.environment >= 0) {
         const DEnv& env = S.envs[l.environment];
         const DTexture t = S.textures[env.tex];
         const int idx = l.nguide ? sample_discrete_guided(cdf, l.ncdf, rel, S.guide_t + l.guide_offset,
@@ -507,6 +515,7 @@ __device__ __forceinline__ bool after_weight(const DParams& P, Path& st) {
 }
 // walk the light list: environment terms are added in place, an instance light starts its
 // query chain; after the last light the one-sample MIS weight is applied (src/trace.jl:386-397)
+template <int F>
 __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P, Path& st) {
     for (;;) {
         st.li += 1;
@@ -523,19 +532,21 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
             st.phase = PH_LIGHT;
             return false;
         }
-        if (l.environment >= 0) st.pdf += env_light_pdf(S, l, st.d);
+        if ((F & FT_ENV) && l.environment >= 0) st.pdf += env_light_pdf(S, l, st.d);
     }
 }
+template <int F>
 __device__ __forceinline__ bool begin_light_pdf(const DScene& S, const DParams& P, Path& st) {
     st.pdf = 0.0f;
     st.li = -1;
-    return light_advance(S, P, st);
+    return light_advance<F>(S, P, st);
 }
 // one intersect_instance_bvh result of the instance-light loop (src/trace.jl:1024-1044)
+template <int F>
 __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Path& st, const Hit& h) {
     if (h.hit) {
         const DLight l = S.lights[st.li];
-        v3 lposition = eval_position(S, l.instance, h.elem, V2(h.u, h.v));
+        v3 lposition = eval_position<F>(S, l.instance, h.elem, V2(h.u, h.v));
         v3 lnormal = eval_element_normal(S, l.instance, h.elem);
         const float area = S.cdf[l.cdf_offset + l.ncdf - 1];
         v3 dd = lposition - st.o;
@@ -544,7 +555,7 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
         if (++st.lcount < 100) return false;
     }
     st.pdf += st.lpdf;
-    return light_advance(S, P, st);
+    return light_advance<F>(S, P, st);
 }
 
 // trace_path's bounce body after the closest-hit query (src/trace.jl:298-453)
@@ -570,14 +581,15 @@ __device__ __forceinline__ void aov_update(const Aov& a, v3 ta, v3 tn) {
     p[9 * BLOCK] = p[9 * BLOCK] * omw + tn.z * a.w;
 }
 
+template <int F>
 __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const Aov& aov,
                                          unsigned& shades) {
     if (!isec.hit) {
-        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment(S, st.d);
+        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
         return true;
     }
     bool in_volume = false;
-    if (st.flags & F_VOLUME) {  // :307-326
+    if ((F & FT_MAT) && (st.flags & F_VOLUME)) {  // :307-326 (volumes need a non-matte material)
         float rl = rand1f(st.rng), rd = rand1f(st.rng);
         float distance = sample_transmittance(st.vol.density, isec.t, rl, rd);
         v3 tr = eval_transmittance(st.vol.density, distance);
@@ -589,13 +601,13 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
     if (!in_volume) {  // surface (:328-423)
         v3 outgoing = -st.d;
         Shading sh;
-        eval_shading(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
+        eval_shading<F>(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
         shades++;
         if (P.nocaustics) {
             st.max_roughness = jl_max(sh.mat.roughness, st.max_roughness);
             sh.mat.roughness = st.max_roughness;
         }
-        if (sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
+        if ((F & FT_OPAC) && sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
             if (st.opbounce > 128) return true;
             st.opbounce += 1;
             st.o = sh.position + st.d * 0.01f;
@@ -617,7 +629,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
             } else {
                 float rl = rand1f(st.rng), rel = rand1f(st.rng);
                 v2 ruv = rand2f(st.rng);
-                incoming = sample_lights(S, sh.position, rl, rel, ruv);
+                incoming = sample_lights<F>(S, sh.position, rl, rel, ruv);
             }
             if (is_zero(incoming)) return true;
             st.weight = st.weight * eval_bsdfcos(sh.mat, sh.normal, outgoing, incoming);
@@ -644,7 +656,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
         }
         st.o = sh.position;
         st.d = incoming;
-        return delta ? after_weight(P, st) : begin_light_pdf(S, P, st);
+        return delta ? after_weight(P, st) : begin_light_pdf<F>(S, P, st);
     }
     // volume scattering (:424-453)
     v3 outgoing = -st.d;
@@ -657,28 +669,29 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
     } else {
         float rl = rand1f(st.rng), rel = rand1f(st.rng);
         v2 ruv = rand2f(st.rng);
-        incoming = sample_lights(S, position, rl, rel, ruv);
+        incoming = sample_lights<F>(S, position, rl, rel, ruv);
     }
     if (is_zero(incoming)) return true;
     st.weight = st.weight * eval_scattering(st.vol, outgoing, incoming);
     st.pb = sample_scattering_pdf(st.vol, outgoing, incoming);
     st.o = position;
     st.d = incoming;
-    return begin_light_pdf(S, P, st);
+    return begin_light_pdf<F>(S, P, st);
 }
 
 // trace_naive's bounce body after the closest-hit query (src/trace.jl:490-569)
+template <int F>
 __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const Aov& aov,
                                           unsigned& shades) {
     if (!isec.hit) {
-        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment(S, st.d);
+        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
         return true;
     }
     v3 outgoing = -st.d;
     Shading sh;
-    eval_shading(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
+    eval_shading<F>(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
     shades++;
-    if (sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
+    if ((F & FT_OPAC) && sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
         if (st.opbounce > 128) return true;
         st.opbounce += 1;
         st.o = sh.position + st.d * 0.01f;
@@ -809,7 +822,7 @@ __device__ __forceinline__ void publish_tile(const DAccum& A, int t, int c) {
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
 // mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
-template <int SAMPLER, int RING, bool OVF, int COUNT>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
                                            int* stack) {
     const int lane = threadIdx.x & 63;
@@ -891,7 +904,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (np >= nn) { steps_p++; lanes_p += np; } else { steps_n++; lanes_n += nn; }
 #endif
             if (np >= nn) {
-                if (T.nprim > 0) prim_step<COUNT>(S, T, cnt);
+                if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
             } else {
                 if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT>(S, T, stack, pixel, cnt);
             }
@@ -908,20 +921,20 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             bool done;
 #if JT_STAMPS
             unsigned long long s0 = __builtin_amdgcn_s_memtime();
-            if (light) done = light_hit(S, P, st, query_hit(T));
+            if (light) done = light_hit<F>(S, P, st, query_hit(T));
             unsigned long long s1 = __builtin_amdgcn_s_memtime();
             if (!light) {
-                if (SAMPLER == 2) done = naive_hit(S, P, st, query_hit(T), aov, cnt.shades);
-                else done = path_hit(S, P, st, query_hit(T), aov, cnt.shades);
+                if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
+                else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
             }
             unsigned long long s2 = __builtin_amdgcn_s_memtime();
             if (__ballot(light)) { t_lhit += s1 - s0; n_lhit++; }
             if (__ballot(!light)) { t_phit += s2 - s1; n_phit++; }
             if (__ballot(done)) n_fin++;
 #else
-            if (light) done = light_hit(S, P, st, query_hit(T));
-            else if (SAMPLER == 2) done = naive_hit(S, P, st, query_hit(T), aov, cnt.shades);
-            else done = path_hit(S, P, st, query_hit(T), aov, cnt.shades);
+            if (light) done = light_hit<F>(S, P, st, query_hit(T));
+            else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
+            else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
 #endif
             if (done) {
                 // trace_sample epilogue (src/trace.jl:625-648)
@@ -1021,16 +1034,16 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
 
 // HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS.
-template <int SAMPLER, int RING, bool OVF, int COUNT>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     __shared__ int lds_stack[RING * BLOCK];
-    trace_body<SAMPLER, RING, OVF, COUNT>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
+    trace_body<SAMPLER, RING, OVF, COUNT, F>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
 }
 
 // LDS mode (small scenes): the workgroup stages the scene blob into LDS once; every node,
 // instance, primitive and shading record is then a ds_read instead of a vector-memory load
 // through the TA/TD path (the measured limiter of the HBM-mode kernel).
-template <int SAMPLER, int RING, bool OVF, int COUNT>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     extern __shared__ uint4 dyn_lds[];
     uint4* blob = dyn_lds + (RING * BLOCK) / 4;
@@ -1054,12 +1067,12 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene
     L.materials = reinterpret_cast<const DMaterial*>(blob + S.o_materials);
     L.lights = reinterpret_cast<const DLight*>(blob + S.o_lights);
     L.cdf = reinterpret_cast<const float*>(blob + S.o_cdf);
-    trace_body<SAMPLER, RING, OVF, COUNT>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+    trace_body<SAMPLER, RING, OVF, COUNT, F>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of
 // tiles), each wave then pulls work units until the launch's units are exhausted.
-template <int SAMPLER, int RING, bool OVF, int COUNT>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
     const int tiles = ((P.width + 7) / 8) * ((P.height + 7) / 8);
     const int want = (tiles + BLOCK / 64 - 1) / (BLOCK / 64);
@@ -1067,32 +1080,39 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
     hipError_t e;
     if (S.blob_n16 > 0) {
         const size_t lds = (size_t)RING * BLOCK * 4 + (size_t)S.blob_n16 * 16;
-        const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT>;
+        const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>;
         if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
         const int nwg = std::min(want, per_cu * cus);
-        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
+        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
     } else {
-        const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT>;
+        const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT, F>;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
         const int nwg = std::min(want, per_cu * cus);
-        hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
+        hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
     }
     return hipGetLastError();
 }
 
-// stack configurations: the whole bound in a 16-entry LDS ring, or a RING-entry ring + HBM
+// Stack configurations: the whole bound in a 16-entry LDS ring, or a RING-entry ring + HBM.
+// Feature specialisations: FT_NONE for scenes without any feature bit (16-entry ring only),
+// FT_ALL for everything else.
+#ifndef JT_ONE_FEAT
+#define JT_ONE_FEAT FT_NONE
+#endif
 template <int SAMPLER, int COUNT>
-hipError_t launch_s(int need, int ring, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A,
+hipError_t launch_s(int need, int ring, int feat, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A,
                     hipStream_t st, int cus) {
 #if JT_ONE_VARIANT  // compile-time experiments only (make quick-usage): one kernel instance
     (void)need;
     (void)ring;
-    return launch_t<1, 16, false, 0>(S, P, s0, s1, A, st, cus);
+    (void)feat;
+    return launch_t<1, 16, false, 0, JT_ONE_FEAT>(S, P, s0, s1, A, st, cus);
 #else
-    if (need <= 16) return launch_t<SAMPLER, 16, false, COUNT>(S, P, s0, s1, A, st, cus);
-    if (ring <= 16) return launch_t<SAMPLER, 16, true, COUNT>(S, P, s0, s1, A, st, cus);
-    return launch_t<SAMPLER, 32, true, COUNT>(S, P, s0, s1, A, st, cus);
+    if (need <= 16 && feat == FT_NONE) return launch_t<SAMPLER, 16, false, COUNT, FT_NONE>(S, P, s0, s1, A, st, cus);
+    if (need <= 16) return launch_t<SAMPLER, 16, false, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
+    if (ring <= 16) return launch_t<SAMPLER, 16, true, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
+    return launch_t<SAMPLER, 32, true, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
 #endif
 }
 
@@ -1114,6 +1134,7 @@ struct jt_ctx {
     int tiles = 0;   // 8x8 pixel tiles
     int stack = 16;  // stack bound of the scene (entries); > 16: LDS ring of `ring` + HBM overflow
     int ring = 16;
+    int feat = FT_ALL;  // scene feature bits (kernel specialisation, see jt_device.h)
     int first = -1, next = 0;  // running-mean origin and next expected sample
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     size_t lds_scene_bytes = 0;  // > 0: small-scene LDS mode
@@ -1322,6 +1343,25 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     c->batch = params->batch;
     c->sampler = params->sampler;
     c->stack = need;
+    {  // scene feature bits (jt_device.h): scenes with none of them run the FT_NONE kernel
+        int f = scene->nenvironments > 0 ? FT_ENV : 0;
+        for (int k = 0; k < scene->nmaterials; k++) {
+            const jt_material& m = scene->materials[k];
+            if (m.type != JT_MATTE) f |= FT_MAT;
+            if (m.emission_tex >= 0 || m.color_tex >= 0 || m.roughness_tex >= 0 || m.scattering_tex >= 0 ||
+                m.normal_tex >= 0)
+                f |= FT_TEX;
+            if (m.opacity < 1) f |= FT_OPAC;
+        }
+        for (int k = 0; k < scene->nshapes; k++) {
+            const jt_shape& sh = scene->shapes[k];
+            if (sh.nquads > 0) f |= FT_QUAD;
+            if (sh.nnormals > 0 || sh.ntexcoords > 0 || sh.ncolors > 0) f |= FT_ATTR;
+        }
+        if (f & (FT_TEX | FT_ATTR)) f |= FT_OPAC;  // texture / vertex-color alpha
+        const char* fe = std::getenv("JT_FEATURES");
+        c->feat = (f == FT_NONE && !(fe && std::strcmp(fe, "all") == 0)) ? FT_NONE : FT_ALL;
+    }
     if (const char* r = std::getenv("JT_LDS_STACK")) c->ring = std::atoi(r) > 16 ? 32 : 16;
     auto bail = [&](int status) {
         jt_destroy(c);
@@ -1710,11 +1750,11 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
     if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if (c->sampler == JT_SAMPLER_NAIVE)
-        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<2, 0>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->feat, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<2, 0>(c->stack, c->ring, c->feat, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     else
-        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<1, 0>(c->stack, c->ring, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->feat, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<1, 0>(c->stack, c->ring, c->feat, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipEventSynchronize(c->ev1)) != hipSuccess) return hip_fail(e, "trace kernel");
@@ -1828,10 +1868,10 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     const int ring = ovf ? c->ring : 16;
     char tmp[512];
     std::snprintf(tmp, sizeof tmp,
-                  "kernel=%s<%d,%d,%s,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
+                  "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
                   "wait_lanes=%d chunk=%d tiles=%d block=%d",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
-                  ring, ovf ? "true" : "false", c->count, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
+                  ring, ovf ? "true" : "false", c->count, (!ovf && c->feat == FT_NONE) ? FT_NONE : FT_ALL, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
                   c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.chunk, c->tiles, BLOCK);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;

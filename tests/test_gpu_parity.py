@@ -144,6 +144,32 @@ def test_lds_and_hbm_scene_modes_bitwise_equal(gpu, abi, lib, cornell_abi, sampl
 
 
 @pytest.mark.parametrize("sampler", [1, 2])
+@pytest.mark.parametrize("lds", ["65536", "0"])
+def test_feature_specialisation_bitwise_equal(gpu, abi, lib, cornell_abi, sampler, lds, monkeypatch):
+    """Cornellbox has no scene feature bit, so it runs the FT_NONE kernel; the general FT_ALL
+    kernel (JT_FEATURES=all) must give the same bits, counters included."""
+    from jtrace import trace
+    bvh = trace.make_scene_bvh(cornell_abi, False, lib)
+    lights = trace.make_trace_lights(cornell_abi, lib)
+    p = make_params(abi, resolution=80, samples=4, sampler=sampler)
+    monkeypatch.setenv("JT_LDS_SCENE", lds)
+    outs = []
+    for feat in ("auto", "all"):
+        monkeypatch.setenv("JT_FEATURES", feat)
+        st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
+        st.set_counters(1)
+        st.trace_range(0, 4)
+        outs.append((st.get_image(), st.get_aovs(), st.counters(), st.describe()))
+        st.close()
+    assert ",0> " in outs[0][3] and ",63> " in outs[1][3], (outs[0][3], outs[1][3])
+    assert np.array_equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert np.array_equal(a, b)
+    for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades"):
+        assert outs[0][2][k] == outs[1][2][k], k
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
 def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sampler, monkeypatch):
     """Work units = (sample chunk, 8x8 tile), fetched dynamically by waves: a tile's chunks are
     accumulated in order (cross-XCD release/acquire), so any chunk size gives the same bits."""
