@@ -141,6 +141,8 @@ struct DParams {
     int envhidden, tentfilter, nocaustics;
     int first;  // running-mean origin: weight of sample s is 1/(s - first + 1)
     int wait_lanes;
+    int light_lanes;  // path sampler: run a light-hit step inside the traversal phase once this
+                      // many lanes wait on a sample_lights_pdf query result (65: never)
     int chunk;  // samples per work unit (a tile's chunks run in order)
     unsigned long long seed;
 };

@@ -479,7 +479,7 @@ __device__ __forceinline__ float env_light_pdf(const DScene& S, const DLight l, 
 // query (PH_SCENE) or one intersect_instance_bvh query of sample_lights_pdf (PH_LIGHT) —
 // which the traversal phase then advances (node_step / prim_step). Float operations and RNG draws happen
 // in exactly the reference's order; only where the lane waits between them changes.
-enum : int { PH_SCENE = 0, PH_LIGHT = 1 };
+enum : int { PH_SCENE = 0, PH_LIGHT = 1, PH_FINISH = 2 };  // PH_FINISH: path done, sample not yet accumulated
 enum : int { F_HIT = 1, F_VOLUME = 2 };
 
 struct Path {
@@ -891,13 +891,38 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         // Each iteration runs ONE step kind — primitive tests or stack pops — picked by lane
         // majority (a wave-uniform branch), so the SIMD executes one code path per iteration.
         // A lane's own sequence of steps is unchanged: it only waits while the other kind runs.
+        // Light-hit steps (path sampler, scenes without environments, whose light_hit is short):
+        // a lane whose sample_lights_pdf query has finished does not wait for the shading
+        // phase — once enough such lanes gather (or nothing else is left to step) the wave runs
+        // light_hit on them and their next query starts at once.
+        constexpr bool LSTEP = SAMPLER == 1 && !(F & FT_ENV);
         for (;;) {
             const bool wantp = T.nprim > 0;
             const bool wantn = T.nprim == 0 && T.sp > 0;
+            const bool waiting = (T.sp | T.nprim) == 0;
             const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
             const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
-            const int nw = lane_count(__builtin_amdgcn_ballot_w64((T.sp | T.nprim) == 0));
+            int nw = lane_count(__builtin_amdgcn_ballot_w64(waiting));
             const int nb = np + nn;
+            if (LSTEP) {
+                const bool wantl = waiting && st.phase == PH_LIGHT;
+                const int nl = lane_count(__builtin_amdgcn_ballot_w64(wantl));
+                if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
+                    if (wantl) {
+                        if (light_hit<F>(S, P, st, query_hit(T))) {
+                            st.phase = PH_FINISH;
+                        } else if (st.phase == PH_LIGHT) {
+                            cnt.light_queries++;
+                            query_begin(T, st.lq, st.d, (T_INST << 30) | (unsigned)S.lights[st.li].instance, stack);
+                        } else {
+                            cnt.rays++;
+                            query_begin(T, st.o, st.d, T_TLAS << 30, stack);
+                        }
+                    }
+                    continue;
+                }
+                nw -= nl;
+            }
             if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
 #if JT_STAMPS
             n_trav++;
@@ -923,7 +948,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             unsigned long long s0 = __builtin_amdgcn_s_memtime();
             if (light) done = light_hit<F>(S, P, st, query_hit(T));
             unsigned long long s1 = __builtin_amdgcn_s_memtime();
-            if (!light) {
+            if (LSTEP && st.phase == PH_FINISH) done = true;
+            else if (!light) {
                 if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
                 else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
             }
@@ -932,7 +958,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (__ballot(!light)) { t_phit += s2 - s1; n_phit++; }
             if (__ballot(done)) n_fin++;
 #else
-            if (light) done = light_hit<F>(S, P, st, query_hit(T));
+            if (LSTEP && st.phase == PH_FINISH) done = true;
+            else if (light) done = light_hit<F>(S, P, st, query_hit(T));
             else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
             else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
 #endif
@@ -1685,8 +1712,13 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.chunk = 0;  // 0: per launch, a quarter of its samples within [8, 64] (enough units per wave)
     if (const char* ch = std::getenv("JT_CHUNK")) P.chunk = std::max(1, std::atoi(ch));
     c->chunk = P.chunk;
-    P.wait_lanes = 40;
+    // measured best (cornellbox): 40 waiting lanes per shading phase; 48 with
+    // light-hit steps in the traversal phase (they take the light queries out of the phases)
+    const bool lstep = c->sampler != JT_SAMPLER_NAIVE && c->feat == FT_NONE && c->stack <= 16;  // the FT_NONE kernel
+    P.wait_lanes = lstep ? 48 : 40;
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
+    P.light_lanes = 2;
+    if (const char* ll = std::getenv("JT_LIGHT_LANES")) P.light_lanes = std::max(1, std::min(65, std::atoi(ll)));
 
     // accumulators (make_trace_state: zeroed) + counters
     const size_t np = (size_t)W * (size_t)H;
@@ -1869,10 +1901,10 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     char tmp[512];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d chunk=%d tiles=%d block=%d",
+                  "wait_lanes=%d light_lanes=%d chunk=%d tiles=%d block=%d",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, (!ovf && c->feat == FT_NONE) ? FT_NONE : FT_ALL, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
-                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.chunk, c->tiles, BLOCK);
+                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->tiles, BLOCK);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;
 }
