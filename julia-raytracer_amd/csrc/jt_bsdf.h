@@ -322,6 +322,9 @@ __device__ __forceinline__ float sample_refractive_delta_pdf(float ior, v3 n, v3
 }
 
 // ---------------------------------------------------------------- dispatch (src/trace.jl)
+// The dispatchers take the kernel's scene feature bits (jt_device.h): without FT_VOL a scene has
+// no refractive/subsurface/volumetric material, so those cases are unreachable and compiled out.
+template <int F>
 __device__ __forceinline__ v3 eval_bsdfcos(const MatPoint& m, v3 n, v3 o, v3 i) {  // :692-755
     if (m.roughness == 0) return V3(0, 0, 0);
     switch (m.type) {
@@ -330,10 +333,11 @@ __device__ __forceinline__ v3 eval_bsdfcos(const MatPoint& m, v3 n, v3 o, v3 i) 
         case M_REFLECTIVE: return eval_reflective(m.color, m.roughness, n, o, i);
         case M_TRANSPARENT: return eval_transparent(m.color, m.ior, m.roughness, n, o, i);
         case M_REFRACTIVE:
-        case M_SUBSURFACE: return eval_refractive(m.ior, m.roughness, n, o, i);
+        case M_SUBSURFACE: return (F & FT_VOL) ? eval_refractive(m.ior, m.roughness, n, o, i) : V3(0, 0, 0);
         default: return V3(0, 0, 0);
     }
 }
+template <int F>
 __device__ __forceinline__ v3 sample_bsdfcos(const MatPoint& m, v3 n, v3 o, float rnl, v2 rn) {  // :780-849
     if (m.roughness == 0) return V3(0, 0, 0);
     switch (m.type) {
@@ -342,10 +346,11 @@ __device__ __forceinline__ v3 sample_bsdfcos(const MatPoint& m, v3 n, v3 o, floa
         case M_REFLECTIVE: return sample_reflective(m.roughness, n, o, rn);
         case M_TRANSPARENT: return sample_transparent(m.ior, m.roughness, n, o, rnl, rn);
         case M_REFRACTIVE:
-        case M_SUBSURFACE: return sample_refractive(m.ior, m.roughness, n, o, rnl, rn);
+        case M_SUBSURFACE: return (F & FT_VOL) ? sample_refractive(m.ior, m.roughness, n, o, rnl, rn) : V3(0, 0, 0);
         default: return V3(0, 0, 0);
     }
 }
+template <int F>
 __device__ __forceinline__ float sample_bsdfcos_pdf(const MatPoint& m, v3 n, v3 o, v3 i) {  // :874-943
     if (m.roughness == 0) return 0;
     switch (m.type) {
@@ -354,36 +359,40 @@ __device__ __forceinline__ float sample_bsdfcos_pdf(const MatPoint& m, v3 n, v3 
         case M_REFLECTIVE: return sample_reflective_pdf(m.roughness, n, o, i);
         case M_TRANSPARENT: return sample_transparent_pdf(m.ior, m.roughness, n, o, i);
         case M_REFRACTIVE:
-        case M_SUBSURFACE: return sample_refractive_pdf(m.ior, m.roughness, n, o, i);
+        case M_SUBSURFACE: return (F & FT_VOL) ? sample_refractive_pdf(m.ior, m.roughness, n, o, i) : 0.0f;
         default: return 0;
     }
 }
+template <int F>
 __device__ __forceinline__ v3 eval_delta(const MatPoint& m, v3 n, v3 o, v3 i) {  // :757-778
     if (m.roughness != 0) return V3(0, 0, 0);
     switch (m.type) {
         case M_REFLECTIVE: return eval_reflective_delta(m.color, n, o, i);
         case M_TRANSPARENT: return eval_transparent_delta(m.color, m.ior, n, o, i);
-        case M_REFRACTIVE: return eval_refractive_delta(m.ior, n, o, i);
-        case M_VOLUMETRIC: return dot(n, i) * dot(n, o) >= 0 ? V3(0, 0, 0) : V3(1, 1, 1);  // passthrough
+        case M_REFRACTIVE: return (F & FT_VOL) ? eval_refractive_delta(m.ior, n, o, i) : V3(0, 0, 0);
+        case M_VOLUMETRIC:  // passthrough
+            return ((F & FT_VOL) && !(dot(n, i) * dot(n, o) >= 0)) ? V3(1, 1, 1) : V3(0, 0, 0);
         default: return V3(0, 0, 0);
     }
 }
+template <int F>
 __device__ __forceinline__ v3 sample_delta(const MatPoint& m, v3 n, v3 o, float rnl) {  // :851-872
     if (m.roughness != 0) return V3(0, 0, 0);
     switch (m.type) {
         case M_REFLECTIVE: return reflect(o, up_normal(n, o));
         case M_TRANSPARENT: return sample_transparent_delta(m.ior, n, o, rnl);
-        case M_REFRACTIVE: return sample_refractive_delta(m.ior, n, o, rnl);
+        case M_REFRACTIVE: return (F & FT_VOL) ? sample_refractive_delta(m.ior, n, o, rnl) : V3(0, 0, 0);
         case M_VOLUMETRIC: return -o;
         default: return V3(0, 0, 0);
     }
 }
+template <int F>
 __device__ __forceinline__ float sample_delta_pdf(const MatPoint& m, v3 n, v3 o, v3 i) {  // :945-966
     if (m.roughness != 0) return 0;
     switch (m.type) {
         case M_REFLECTIVE: return dot(n, i) * dot(n, o) <= 0 ? 0.0f : 1.0f;
         case M_TRANSPARENT: return sample_transparent_delta_pdf(m.ior, n, o, i);
-        case M_REFRACTIVE: return sample_refractive_delta_pdf(m.ior, n, o, i);
+        case M_REFRACTIVE: return (F & FT_VOL) ? sample_refractive_delta_pdf(m.ior, n, o, i) : 0.0f;
         case M_VOLUMETRIC: return dot(n, i) * dot(n, o) >= 0 ? 0.0f : 1.0f;
         default: return 0;
     }

@@ -39,16 +39,18 @@ enum { KIND_TRI = 0, KIND_QUAD = 1 };
 // Scene feature bits of a kernel specialisation (chosen per scene by jt_create): a kernel built
 // without a bit assumes the scene has none of it, so the branches it guards are compiled out.
 // FT_ALL is the general kernel; FT_NONE serves scenes of matte triangles without textures,
-// vertex attributes, environments or opacity (cornellbox). Results are bit-identical.
+// vertex attributes, environments or opacity (cornellbox); jt_create picks the smallest compiled
+// mask that covers the scene (jt_trace.hip, launch_s). Results are bit-identical.
 enum : int {
     FT_TEX = 1,    // material textures (incl. normal maps)
     FT_ATTR = 2,   // shape normals / texcoords / colors
     FT_QUAD = 4,   // quad shapes
-    FT_MAT = 8,    // materials other than matte (and with them volumes)
+    FT_MAT = 8,    // materials other than matte
     FT_ENV = 16,   // environments (escaped rays, environment lights)
-    FT_OPAC = 32,  // opacity < 1 possible (material opacity, texture or vertex-color alpha)
+    FT_OPAC = 32,  // opacity < 1 possible (material opacity, color-texture or vertex-color alpha)
+    FT_VOL = 64,   // refractive / subsurface / volumetric materials (the volume stack)
     FT_NONE = 0,
-    FT_ALL = 63
+    FT_ALL = 127
 };
 struct alignas(16) DShape {
     int kind, blas_root, prim_base, idx_base;

@@ -212,7 +212,7 @@ __device__ __forceinline__ void eval_shading(const DScene& S, int inst, int elem
     p.scattering = V3(m.scattering[0], m.scattering[1], m.scattering[2]) * xyz(scattering_tex);
     p.scanisotropy = m.scanisotropy;
     p.trdepth = m.trdepth;
-    if (mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE) {
+    if ((F & FT_VOL) && (mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE)) {
         p.density = V3(-jl_log(jl_clamp(p.color.x, 0.0001f, 1.0f)) / p.trdepth,
                        -jl_log(jl_clamp(p.color.y, 0.0001f, 1.0f)) / p.trdepth,
                        -jl_log(jl_clamp(p.color.z, 0.0001f, 1.0f)) / p.trdepth);
@@ -589,7 +589,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
         return true;
     }
     bool in_volume = false;
-    if ((F & FT_MAT) && (st.flags & F_VOLUME)) {  // :307-326 (volumes need a non-matte material)
+    if ((F & FT_VOL) && (st.flags & F_VOLUME)) {  // :307-326 (volumes need a volume material)
         float rl = rand1f(st.rng), rd = rand1f(st.rng);
         float distance = sample_transmittance(st.vol.density, isec.t, rl, rd);
         v3 tr = eval_transmittance(st.vol.density, distance);
@@ -625,25 +625,25 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
             if (rand1f(st.rng) < 0.5f) {
                 float rnl = rand1f(st.rng);
                 v2 rn = rand2f(st.rng);
-                incoming = sample_bsdfcos(sh.mat, sh.normal, outgoing, rnl, rn);
+                incoming = sample_bsdfcos<F>(sh.mat, sh.normal, outgoing, rnl, rn);
             } else {
                 float rl = rand1f(st.rng), rel = rand1f(st.rng);
                 v2 ruv = rand2f(st.rng);
                 incoming = sample_lights<F>(S, sh.position, rl, rel, ruv);
             }
             if (is_zero(incoming)) return true;
-            st.weight = st.weight * eval_bsdfcos(sh.mat, sh.normal, outgoing, incoming);
-            st.pb = sample_bsdfcos_pdf(sh.mat, sh.normal, outgoing, incoming);
+            st.weight = st.weight * eval_bsdfcos<F>(sh.mat, sh.normal, outgoing, incoming);
+            st.pb = sample_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
         } else {
             float rnl = rand1f(st.rng);
-            incoming = sample_delta(sh.mat, sh.normal, outgoing, rnl);
-            v3 f = eval_delta(sh.mat, sh.normal, outgoing, incoming);
-            float pd = sample_delta_pdf(sh.mat, sh.normal, outgoing, incoming);
+            incoming = sample_delta<F>(sh.mat, sh.normal, outgoing, rnl);
+            v3 f = eval_delta<F>(sh.mat, sh.normal, outgoing, incoming);
+            float pd = sample_delta_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
             st.weight = (st.weight * f) / pd;
         }
         // volume stack push/pop (:405-421); independent of the weight update it follows
         const int mtype = sh.mat.type;
-        if ((mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE) &&
+        if ((F & FT_VOL) && (mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE) &&
             dot(sh.normal, outgoing) * dot(sh.normal, incoming) < 0) {
             if (!(st.flags & F_VOLUME)) {
                 st.flags |= F_VOLUME;  // eval_material again: only the volume fields are kept
@@ -708,16 +708,16 @@ __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Pat
     if (sh.mat.roughness != 0) {
         float rnl = rand1f(st.rng);
         v2 rn = rand2f(st.rng);
-        incoming = sample_bsdfcos(sh.mat, sh.normal, outgoing, rnl, rn);
+        incoming = sample_bsdfcos<F>(sh.mat, sh.normal, outgoing, rnl, rn);
         if (is_zero(incoming)) return true;
-        f = eval_bsdfcos(sh.mat, sh.normal, outgoing, incoming);
-        p = sample_bsdfcos_pdf(sh.mat, sh.normal, outgoing, incoming);
+        f = eval_bsdfcos<F>(sh.mat, sh.normal, outgoing, incoming);
+        p = sample_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
     } else {
         float rnl = rand1f(st.rng);
-        incoming = sample_delta(sh.mat, sh.normal, outgoing, rnl);
+        incoming = sample_delta<F>(sh.mat, sh.normal, outgoing, rnl);
         if (is_zero(incoming)) return true;
-        f = eval_delta(sh.mat, sh.normal, outgoing, incoming);
-        p = sample_delta_pdf(sh.mat, sh.normal, outgoing, incoming);
+        f = eval_delta<F>(sh.mat, sh.normal, outgoing, incoming);
+        p = sample_delta_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
     }
     st.weight = (st.weight * f) / p;
     st.o = sh.position;
@@ -1099,46 +1099,72 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of
 // tiles), each wave then pulls work units until the launch's units are exhausted.
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
+// LDSK: the specialisation also has an LDS-mode kernel (the large-scene masks run in HBM mode).
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool LDSK = true>
 hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
     const int tiles = ((P.width + 7) / 8) * ((P.height + 7) / 8);
     const int want = (tiles + BLOCK / 64 - 1) / (BLOCK / 64);
     int per_cu = 0;
     hipError_t e;
-    if (S.blob_n16 > 0) {
+    if constexpr (LDSK) {
+        if (S.blob_n16 > 0) {
         const size_t lds = (size_t)RING * BLOCK * 4 + (size_t)S.blob_n16 * 16;
         const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>;
         if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
         const int nwg = std::min(want, per_cu * cus);
         hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
-    } else {
-        const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT, F>;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-        const int nwg = std::min(want, per_cu * cus);
-        hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
+        return hipGetLastError();
+        }
     }
+    const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT, F>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    const int nwg = std::min(want, per_cu * cus);
+    hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
     return hipGetLastError();
 }
 
-// Stack configurations: the whole bound in a 16-entry LDS ring, or a RING-entry ring + HBM.
-// Feature specialisations: FT_NONE for scenes without any feature bit (16-entry ring only),
-// FT_ALL for everything else.
+// Feature specialisations compiled per stack configuration (besides FT_ALL): FT_NONE for small
+// scenes with a 16-entry stack (cornellbox), and three masks for large HBM-mode scenes with the
+// ring + HBM overflow stack — textured, attributed meshes (bathroom1), plus environments
+// (ecosys), plus quads (features2).
+constexpr int FT_MESH = FT_TEX | FT_ATTR | FT_MAT | FT_OPAC;
+constexpr int FT_MESH_ENV = FT_MESH | FT_ENV;
+constexpr int FT_MESH_ENV_QUAD = FT_MESH_ENV | FT_QUAD;
+// the kernel mask a scene with feature bits `feat` runs with (the smallest compiled superset)
+int kernel_mask(int feat, int need, int ring, bool lds) {
+    if (need <= 16) return feat == FT_NONE ? FT_NONE : FT_ALL;
+    if (ring > 16 || lds) return FT_ALL;
+    for (int m : {FT_MESH, FT_MESH_ENV, FT_MESH_ENV_QUAD})
+        if (!(feat & ~m)) return m;
+    return FT_ALL;
+}
 #ifndef JT_ONE_FEAT
 #define JT_ONE_FEAT FT_NONE
 #endif
+// Stack configurations: the whole bound in a 16-entry LDS ring, or a RING-entry ring + HBM.
 template <int SAMPLER, int COUNT>
-hipError_t launch_s(int need, int ring, int feat, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A,
-                    hipStream_t st, int cus) {
+hipError_t launch_s(int need, int ring, int kmask, const DScene& S, const DParams& P, int s0, int s1,
+                    const DAccum& A, hipStream_t st, int cus) {
 #if JT_ONE_VARIANT  // compile-time experiments only (make quick-usage): one kernel instance
     (void)need;
     (void)ring;
-    (void)feat;
+    (void)kmask;
     return launch_t<1, 16, false, 0, JT_ONE_FEAT>(S, P, s0, s1, A, st, cus);
 #else
-    if (need <= 16 && feat == FT_NONE) return launch_t<SAMPLER, 16, false, COUNT, FT_NONE>(S, P, s0, s1, A, st, cus);
-    if (need <= 16) return launch_t<SAMPLER, 16, false, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
-    if (ring <= 16) return launch_t<SAMPLER, 16, true, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
+    if (need <= 16) {
+        if (kmask == FT_NONE) return launch_t<SAMPLER, 16, false, COUNT, FT_NONE>(S, P, s0, s1, A, st, cus);
+        return launch_t<SAMPLER, 16, false, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
+    }
+    if (ring <= 16) {
+        switch (kmask) {
+            case FT_MESH: return launch_t<SAMPLER, 16, true, COUNT, FT_MESH, false>(S, P, s0, s1, A, st, cus);
+            case FT_MESH_ENV: return launch_t<SAMPLER, 16, true, COUNT, FT_MESH_ENV, false>(S, P, s0, s1, A, st, cus);
+            case FT_MESH_ENV_QUAD:
+                return launch_t<SAMPLER, 16, true, COUNT, FT_MESH_ENV_QUAD, false>(S, P, s0, s1, A, st, cus);
+            default: return launch_t<SAMPLER, 16, true, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
+        }
+    }
     return launch_t<SAMPLER, 32, true, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
 #endif
 }
@@ -1161,7 +1187,8 @@ struct jt_ctx {
     int tiles = 0;   // 8x8 pixel tiles
     int stack = 16;  // stack bound of the scene (entries); > 16: LDS ring of `ring` + HBM overflow
     int ring = 16;
-    int feat = FT_ALL;  // scene feature bits (kernel specialisation, see jt_device.h)
+    int feat = FT_ALL;   // scene feature bits (jt_device.h)
+    int kmask = FT_ALL;  // feature mask of the kernel specialisation the scene runs
     int first = -1, next = 0;  // running-mean origin and next expected sample
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     size_t lds_scene_bytes = 0;  // > 0: small-scene LDS mode
@@ -1375,19 +1402,22 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         for (int k = 0; k < scene->nmaterials; k++) {
             const jt_material& m = scene->materials[k];
             if (m.type != JT_MATTE) f |= FT_MAT;
+            if (m.type == JT_REFRACTIVE || m.type == JT_VOLUMETRIC || m.type == JT_SUBSURFACE) f |= FT_VOL;
             if (m.emission_tex >= 0 || m.color_tex >= 0 || m.roughness_tex >= 0 || m.scattering_tex >= 0 ||
                 m.normal_tex >= 0)
                 f |= FT_TEX;
-            if (m.opacity < 1) f |= FT_OPAC;
+            // opacity = m.opacity * color_tex.w * color_shp.w (src/scene.jl:649): a bilinear or
+            // barycentric alpha of 1s need not round to exactly 1, so any color texture counts
+            if (m.opacity < 1 || m.color_tex >= 0) f |= FT_OPAC;
         }
         for (int k = 0; k < scene->nshapes; k++) {
             const jt_shape& sh = scene->shapes[k];
             if (sh.nquads > 0) f |= FT_QUAD;
             if (sh.nnormals > 0 || sh.ntexcoords > 0 || sh.ncolors > 0) f |= FT_ATTR;
+            if (sh.ncolors > 0) f |= FT_OPAC;
         }
-        if (f & (FT_TEX | FT_ATTR)) f |= FT_OPAC;  // texture / vertex-color alpha
         const char* fe = std::getenv("JT_FEATURES");
-        c->feat = (f == FT_NONE && !(fe && std::strcmp(fe, "all") == 0)) ? FT_NONE : FT_ALL;
+        c->feat = (fe && std::strcmp(fe, "all") == 0) ? FT_ALL : f;
     }
     if (const char* r = std::getenv("JT_LDS_STACK")) c->ring = std::atoi(r) > 16 ? 32 : 16;
     auto bail = [&](int status) {
@@ -1714,7 +1744,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     c->chunk = P.chunk;
     // measured best (cornellbox): 40 waiting lanes per shading phase; 48 with
     // light-hit steps in the traversal phase (they take the light queries out of the phases)
-    const bool lstep = c->sampler != JT_SAMPLER_NAIVE && c->feat == FT_NONE && c->stack <= 16;  // the FT_NONE kernel
+    c->kmask = kernel_mask(c->feat, c->stack, c->ring, c->lds_scene_bytes > 0);
+    const bool lstep = c->sampler != JT_SAMPLER_NAIVE && !(c->kmask & FT_ENV);  // LSTEP in trace_body
     P.wait_lanes = lstep ? 48 : 40;
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
     P.light_lanes = 2;
@@ -1782,11 +1813,11 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
     if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if (c->sampler == JT_SAMPLER_NAIVE)
-        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->feat, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<2, 0>(c->stack, c->ring, c->feat, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<2, 0>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     else
-        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->feat, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<1, 0>(c->stack, c->ring, c->feat, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<1, 0>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipEventSynchronize(c->ev1)) != hipSuccess) return hip_fail(e, "trace kernel");
@@ -1903,7 +1934,7 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
                   "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
                   "wait_lanes=%d light_lanes=%d chunk=%d tiles=%d block=%d",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
-                  ring, ovf ? "true" : "false", c->count, (!ovf && c->feat == FT_NONE) ? FT_NONE : FT_ALL, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
+                  ring, ovf ? "true" : "false", c->count, c->kmask, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
                   c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->tiles, BLOCK);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;
