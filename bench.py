@@ -200,7 +200,10 @@ def main():
                 "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
                 "kernel": kernel, "launch": desc, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                 "bytes_per_launch": int(bytes_per_launch),
-                "bytes_per_ray": round(bytes_per_launch / max(1.0, per_launch["rays"]), 1)}
+                "bytes_per_ray": round(bytes_per_launch / max(1.0, per_launch["rays"]), 1),
+                # traversal work per closest-hit query, from the counting pass
+                "per_ray": {k: round(per_launch[k] / max(1.0, per_launch["rays"]), 3)
+                            for k in ("nodes", "instances", "prims", "shades", "light_queries")}}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(sa, jp, W, H, args.cpu_threads, args.cpu_spp)

@@ -513,6 +513,26 @@ __device__ __forceinline__ PrimHit intersect_triangle_e(v3 o, v3 d, float tmin, 
     r.hit = !miss;
     return r;
 }
+// The triangle test without its `t > tmax` rejection (the only use of tmax): hit = every other
+// test passed. tri_hit_before(p, tmax) completes it, so two consecutive primitives can be
+// computed side by side and then accepted in order, each against the tmax the previous one left.
+__device__ __forceinline__ PrimHit intersect_triangle_pre(v3 o, v3 d, float tmin, v3 p1, v3 edge1, v3 edge2) {
+    v3 pvec = cross(d, edge2);
+    float det = dot(edge1, pvec);
+    float inv_det = 1.0f / det;
+    v3 tvec = o - p1;
+    float u = dot(tvec, pvec) * inv_det;
+    v3 qvec = cross(tvec, edge1);
+    float v = dot(d, qvec) * inv_det;
+    float t = dot(edge2, qvec) * inv_det;
+    PrimHit r;
+    r.u = u;
+    r.v = v;
+    r.t = t;
+    r.hit = !((det == 0) | (u < 0 || u > 1) | (v < 0 || u + v > 1) | (t < tmin));
+    return r;
+}
+__device__ __forceinline__ bool tri_hit_before(const PrimHit& p, float tmax) { return p.hit && !(p.t > tmax); }
 // triangle records carry the edges p2 - p1, p3 - p1, precomputed on the host (the same floats)
 __device__ __forceinline__ PrimHit intersect_triangle(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 p2, v3 p3) {
     return intersect_triangle_e(o, d, tmin, tmax, p1, p2 - p1, p3 - p1);

@@ -320,26 +320,44 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     T.low = 0;
 }
 
-// One primitive of the current BLAS leaf (src/bvh.jl:444-484).
+// The current BLAS leaf's next primitive(s), in order (src/bvh.jl:444-484). Triangles go two at a
+// time: both tests are computed side by side (the record after the leaf's last one exists: the
+// array is padded), then accepted in order, the second against the tmax the first left.
 template <int COUNT, int F>
 __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cnt) {
-    if (COUNT) cnt.prims++;
-    PrimHit p;
-    int elem;
     if (!(F & FT_QUAD) || T.cur_kind == KIND_TRI) {
         const float4* r = S.prims + 3 * T.prim;
-        const float4 a = r[0], b = r[1], c = r[2];
-        elem = __float_as_int(a.w);
-        p = intersect_triangle_e(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c));  // (p1, edge1, edge2)
-    } else {
-        const float4* r = S.prims + 4 * T.prim;
-        const float4 a = r[0], b = r[1], c = r[2], d = r[3];
-        elem = __float_as_int(a.w);
-        p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
+        const float4 a = r[0], b = r[1], c = r[2], a2 = r[3], b2 = r[4], c2 = r[5];
+        const PrimHit p1 = intersect_triangle_pre(T.lo, T.ld, ray_eps, xyz(a), xyz(b), xyz(c));
+        const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, xyz(a2), xyz(b2), xyz(c2));
+        const bool two = T.nprim >= 2;
+        if (tri_hit_before(p1, T.tmax)) {
+            T.h_inst = T.cur_inst;
+            T.h_elem = __float_as_int(a.w);
+            T.h_u = p1.u;
+            T.h_v = p1.v;
+            T.tmax = p1.t;
+        }
+        if (two && tri_hit_before(p2, T.tmax)) {
+            T.h_inst = T.cur_inst;
+            T.h_elem = __float_as_int(a2.w);
+            T.h_u = p2.u;
+            T.h_v = p2.v;
+            T.tmax = p2.t;
+        }
+        const int n = two ? 2 : 1;
+        if (COUNT) cnt.prims += n;
+        T.prim += n;
+        T.nprim -= n;
+        return;
     }
+    if (COUNT) cnt.prims++;
+    const float4* r = S.prims + 4 * T.prim;
+    const float4 a = r[0], b = r[1], c = r[2], d = r[3];
+    const PrimHit p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
     if (p.hit) {
         T.h_inst = T.cur_inst;
-        T.h_elem = elem;
+        T.h_elem = __float_as_int(a.w);
         T.h_u = p.u;
         T.h_v = p.v;
         T.tmax = p.t;
@@ -1632,6 +1650,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     build_luts(srgb, bytes);
 
     DScene& S = c->S;
+    // one zero record past the last primitive: prim_step reads the record after a leaf's last
+    for (int q = 0; q < 4; q++) prims.push_back(f4(0, 0, 0, 0));
     std::vector<DNode> nodes(tlas);
     nodes.insert(nodes.end(), blas.begin(), blas.end());
     if ((st = upload(c, nodes, &S.nodes)) || (st = upload(c, tlas_prims, &S.tlas_prims)) || (st = upload(c, prims, &S.prims)) ||
