@@ -320,32 +320,40 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     T.low = 0;
 }
 
-// The current BLAS leaf's next primitive(s), in order (src/bvh.jl:444-484). Triangles go two at a
-// time: both tests are computed side by side (the record after the leaf's last one exists: the
-// array is padded), then accepted in order, the second against the tmax the first left.
+// The current BLAS leaf's next primitive(s), in order (src/bvh.jl:444-484). Triangles go in
+// pairs: both tests are computed side by side (the record after the leaf's last one exists: the
+// array is padded), then accepted in order, the second against the tmax the first left. A
+// second pair runs in the same step when some lane's leaf has more than two left.
+template <int F>
+__device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
+    const float4* r = S.prims + 3 * (T.prim + k);
+    const float4 a = r[0], b = r[1], c = r[2], a2 = r[3], b2 = r[4], c2 = r[5];
+    const PrimHit p1 = intersect_triangle_pre(T.lo, T.ld, ray_eps, xyz(a), xyz(b), xyz(c));
+    const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, xyz(a2), xyz(b2), xyz(c2));
+    if (tri_hit_before(p1, T.tmax)) {
+        T.h_inst = T.cur_inst;
+        T.h_elem = __float_as_int(a.w);
+        T.h_u = p1.u;
+        T.h_v = p1.v;
+        T.tmax = p1.t;
+    }
+    if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax)) {
+        T.h_inst = T.cur_inst;
+        T.h_elem = __float_as_int(a2.w);
+        T.h_u = p2.u;
+        T.h_v = p2.v;
+        T.tmax = p2.t;
+    }
+}
 template <int COUNT, int F>
 __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cnt) {
     if (!(F & FT_QUAD) || T.cur_kind == KIND_TRI) {
-        const float4* r = S.prims + 3 * T.prim;
-        const float4 a = r[0], b = r[1], c = r[2], a2 = r[3], b2 = r[4], c2 = r[5];
-        const PrimHit p1 = intersect_triangle_pre(T.lo, T.ld, ray_eps, xyz(a), xyz(b), xyz(c));
-        const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, xyz(a2), xyz(b2), xyz(c2));
-        const bool two = T.nprim >= 2;
-        if (tri_hit_before(p1, T.tmax)) {
-            T.h_inst = T.cur_inst;
-            T.h_elem = __float_as_int(a.w);
-            T.h_u = p1.u;
-            T.h_v = p1.v;
-            T.tmax = p1.t;
+        tri_pair<F>(S, T, 0);
+        const bool more = T.nprim > 2;
+        if (__builtin_amdgcn_ballot_w64(more)) {
+            if (more) tri_pair<F>(S, T, 2);
         }
-        if (two && tri_hit_before(p2, T.tmax)) {
-            T.h_inst = T.cur_inst;
-            T.h_elem = __float_as_int(a2.w);
-            T.h_u = p2.u;
-            T.h_v = p2.v;
-            T.tmax = p2.t;
-        }
-        const int n = two ? 2 : 1;
+        const int n = T.nprim < 4 ? T.nprim : 4;
         if (COUNT) cnt.prims += n;
         T.prim += n;
         T.nprim -= n;
