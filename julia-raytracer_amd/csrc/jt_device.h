@@ -203,6 +203,18 @@ __device__ __forceinline__ float jl_max(float x, float y) {
     return c ? (__builtin_isnan(x) ? x : y) : (__builtin_isnan(y) ? y : x);
 }
 __device__ __forceinline__ float jl_clamp(float x, float lo, float hi) { return x > hi ? hi : (x < lo ? lo : x); }
+// 1.0f / x, correctly rounded like the IEEE division it replaces: v_rcp_f32 plus one FMA Newton
+// step equals it for every x with a normal exponent below 2^126 (so the reciprocal is normal
+// too) — verified over all 2^32 inputs by scripts/exhaustive/rcp_check.hip on gfx950. Zeros,
+// denormals, |x| >= 2^126, inf and NaN take the division.
+__device__ __forceinline__ float jl_rcp(float x) {
+    const unsigned e = (__float_as_uint(x) >> 23) & 0xffu;
+    if (__builtin_expect(e - 1u < 252u, 1)) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+    }
+    return 1.0f / x;
+}
 __device__ __forceinline__ int jl_clampi(int x, int lo, int hi) { return x > hi ? hi : (x < lo ? lo : x); }
 __device__ __forceinline__ float max3(v3 a) { return jl_max(jl_max(a.x, a.y), a.z); }
 
@@ -499,7 +511,7 @@ struct PrimHit {
 __device__ __forceinline__ PrimHit intersect_triangle_e(v3 o, v3 d, float tmin, float tmax, v3 p1, v3 edge1, v3 edge2) {
     v3 pvec = cross(d, edge2);
     float det = dot(edge1, pvec);
-    float inv_det = 1.0f / det;
+    float inv_det = jl_rcp(det);
     v3 tvec = o - p1;
     float u = dot(tvec, pvec) * inv_det;
     v3 qvec = cross(tvec, edge1);
@@ -519,7 +531,7 @@ __device__ __forceinline__ PrimHit intersect_triangle_e(v3 o, v3 d, float tmin, 
 __device__ __forceinline__ PrimHit intersect_triangle_pre(v3 o, v3 d, float tmin, v3 p1, v3 edge1, v3 edge2) {
     v3 pvec = cross(d, edge2);
     float det = dot(edge1, pvec);
-    float inv_det = 1.0f / det;
+    float inv_det = jl_rcp(det);
     v3 tvec = o - p1;
     float u = dot(tvec, pvec) * inv_det;
     v3 qvec = cross(tvec, edge1);

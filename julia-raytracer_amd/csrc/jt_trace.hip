@@ -300,7 +300,7 @@ __device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T
 __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, int* stack) {
     T.wo = o;
     T.wd = d;
-    T.wdinv = V3(1 / d.x, 1 / d.y, 1 / d.z);  // ray_dinv (src/bvh.jl:322), no guard
+    T.wdinv = V3(jl_rcp(d.x), jl_rcp(d.y), jl_rcp(d.z));  // ray_dinv (src/bvh.jl:322), no guard
     T.lo = o;
     T.ld = d;
     T.ldinv = T.wdinv;
@@ -419,7 +419,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             const fr3 inv = frame_from(it.i0, it.i1, it.i2);
             T.lo = transform_point(inv, T.wo);
             T.ld = transform_vector(inv, T.wd);
-            T.ldinv = V3(1 / T.ld.x, 1 / T.ld.y, 1 / T.ld.z);
+            T.ldinv = V3(jl_rcp(T.ld.x), jl_rcp(T.ld.y), jl_rcp(T.ld.z));
             T.negmask = neg_mask(T.ld);
             T.inst_space = 1;
         }
