@@ -119,6 +119,10 @@ struct DScene {
     // units; -1 = not in the blob). Texels, environments and LUTs stay in HBM.
     const uint4* blob;
     int blob_n16;
+    // HBM mode: nodes [0, nlnodes) — the top of the TLAS, laid out breadth-first — are copied
+    // into LDS by every workgroup and read from there (lnodes)
+    const DNode* lnodes;
+    int nlnodes;
     // traversal-stack overflow (scenes deeper than the LDS ring): ovf_stride entries per pixel
     int* ovf;
     int ovf_stride;

@@ -30,6 +30,12 @@
 #ifndef JT_STAMPS
 #define JT_STAMPS 0
 #endif
+#ifndef JT_NODE_REPEAT
+#define JT_NODE_REPEAT 3
+#endif
+#ifndef JT_FIRST_POP
+#define JT_FIRST_POP 1
+#endif
 
 using namespace jtd;
 
@@ -404,7 +410,7 @@ __device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* 
 // test of its BLAS root are one step: the reference's instance visit pushes nothing but the
 // root (src/bvh.jl:345-351, 502-506), which is then the very next pop, so testing it in the same
 // step visits the same nodes in the same order.
-template <int RING, bool OVF, int COUNT>
+template <int RING, bool OVF, int COUNT, bool NCACHE>
 __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
     const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
     unsigned type = e >> 30, idx = e & IDX_MASK;
@@ -431,7 +437,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         world_ray(T);  // back from an instance: TLAS nodes test the world ray
     }
     const bool blas = type == T_BLAS;
-    const DNode nd = S.nodes[idx];
+    const DNode nd = (NCACHE && (int)idx < S.nlnodes) ? S.lnodes[idx] : S.nodes[idx];
     if (COUNT) cnt.nodes++;
     if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
     const unsigned meta = __float_as_uint(nd.b.w);
@@ -848,7 +854,7 @@ __device__ __forceinline__ void publish_tile(const DAccum& A, int t, int c) {
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
 // mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
                                            int* stack) {
     const int lane = threadIdx.x & 63;
@@ -957,7 +963,12 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (np >= nn) {
                 if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
             } else {
-                if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT>(S, T, stack, pixel, cnt);
+                // JT_NODE_REPEAT pops per node iteration: a lane whose next step is again a
+                // stack pop takes it at once (the same steps in the same per-lane order, less
+                // per-iteration vote and loop overhead)
+#pragma unroll
+                for (int k = 0; k < JT_NODE_REPEAT; k++)
+                    if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE>(S, T, stack, pixel, cnt);
             }
         }
 #if JT_STAMPS
@@ -1028,6 +1039,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                     cnt.rays++;
                     query_begin(T, st.o, st.d, T_TLAS << 30, stack);
                 }
+                // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
+                // where most of the wave's lanes take part, rather than in a sparser traversal step
+                if (JT_FIRST_POP) node_step<RING, OVF, COUNT, NCACHE>(S, T, stack, pixel, cnt);
             }
 #if JT_STAMPS
             t_qb += __builtin_amdgcn_s_memtime() - s3;
@@ -1086,11 +1100,20 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #define JT_WAVES_PER_EU
 #endif
 
-// HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS.
+// HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS. The
+// workgroup first copies the top nlnodes nodes (the breadth-first top of the TLAS, visited by
+// nearly every ray) into dynamic LDS: those node reads then skip the vector-memory path (TA/TD,
+// the measured limiter of this mode).
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     __shared__ int lds_stack[RING * BLOCK];
-    trace_body<SAMPLER, RING, OVF, COUNT, F>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
+    extern __shared__ uint4 node_cache[];
+    const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
+    for (int k = threadIdx.x; k < 2 * S.nlnodes; k += BLOCK) node_cache[k] = src[k];
+    __syncthreads();
+    DScene L = S;
+    L.lnodes = reinterpret_cast<const DNode*>(node_cache);
+    trace_body<SAMPLER, RING, OVF, COUNT, F, true>(L, P, s_begin, s_end, A, lds_stack + threadIdx.x);
 }
 
 // LDS mode (small scenes): the workgroup stages the scene blob into LDS once; every node,
@@ -1120,7 +1143,7 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene
     L.materials = reinterpret_cast<const DMaterial*>(blob + S.o_materials);
     L.lights = reinterpret_cast<const DLight*>(blob + S.o_lights);
     L.cdf = reinterpret_cast<const float*>(blob + S.o_cdf);
-    trace_body<SAMPLER, RING, OVF, COUNT, F>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+    trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of
@@ -1144,9 +1167,11 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
         }
     }
     const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT, F>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    const size_t cache = (size_t)S.nlnodes * sizeof(DNode);
+    if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cache)) != hipSuccess) return e;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, cache) != hipSuccess || per_cu < 1) per_cu = 1;
     const int nwg = std::min(want, per_cu * cus);
-    hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
+    hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), cache, st, S, P, s0, s1, A);
     return hipGetLastError();
 }
 
@@ -1455,8 +1480,28 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         return bail(hip_fail(e, "hipEventCreate"));
 
     // ------------------------------------------------------------- flatten to the HBM layout
-    std::vector<DNode> tlas(std::max(0, bvh->tlas.nnodes));
-    for (int k = 0; k < bvh->tlas.nnodes; k++) tlas[k] = pack_node(bvh->tlas.nodes[k], bvh->tlas.nodes[k].start);
+    // The TLAS is stored breadth-first (sibling pairs stay adjacent, the root stays node 0), so its
+    // top levels are one prefix of the node array — the prefix HBM mode caches in LDS. Storage
+    // order only: the traversal still visits the reference's nodes in the reference's order.
+    std::vector<DNode> tlas;
+    {
+        const int tn = std::max(0, bvh->tlas.nnodes);
+        std::vector<int> order, newidx(tn, -1);
+        if (tn > 0) order.push_back(0);
+        for (size_t q = 0; q < order.size(); q++) {
+            const jt_bvh_node& n = bvh->tlas.nodes[order[q]];
+            if (n.internal) {
+                order.push_back(n.start);
+                order.push_back(n.start + 1);
+            }
+        }
+        for (size_t q = 0; q < order.size(); q++) newidx[order[q]] = (int)q;
+        tlas.resize(order.size());
+        for (size_t q = 0; q < order.size(); q++) {
+            const jt_bvh_node& n = bvh->tlas.nodes[order[q]];
+            tlas[q] = pack_node(n, n.internal ? newidx[n.start] : n.start);
+        }
+    }
     std::vector<int> tlas_prims(bvh->tlas.primitives, bvh->tlas.primitives + bvh->tlas.nprimitives);
     std::vector<DNode> blas;
     std::vector<float4> prims;
@@ -1471,7 +1516,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         DShape& d = shapes[s];
         d.kind = sh.ntriangles ? KIND_TRI : KIND_QUAD;
         const int stride = d.kind == KIND_TRI ? 3 : 4;
-        d.blas_root = bvh->tlas.nnodes + (int)blas.size();  // global index: TLAS nodes come first
+        d.blas_root = (int)tlas.size() + (int)blas.size();  // global index: TLAS nodes come first
         // records are 3 (triangle) or 4 (quad) float4s: align the shape's first record to its
         // stride so prim_base * stride addresses it exactly when shape kinds are mixed
         while (prims.size() % stride) prims.push_back(f4(0, 0, 0, 0));
@@ -1671,7 +1716,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) ||
         (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
         return bail(st);
-    S.tlas_nnodes = bvh->tlas.nnodes;
+    S.tlas_nnodes = (int)tlas.size();
     S.nenvs = scene->nenvironments;
     S.nlights = lights->nlights;
 
@@ -1721,6 +1766,16 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             S.blob_n16 = (int)blob.size();
         }
         c->lds_scene_bytes = S.blob_n16 ? bytes : 0;
+        // HBM mode: cache the breadth-first top of the TLAS in what LDS is left at 4 workgroups
+        // per CU (160 KiB / 4 minus the stack ring and the running means); JT_NODE_CACHE caps it
+        S.lnodes = nullptr;
+        S.nlnodes = 0;
+        if (!S.blob_n16) {
+            const long left = (long)(lds_cu / 4) - (long)base_bytes;
+            long n = std::min<long>((long)tlas.size(), std::max<long>(0, left) / (long)sizeof(DNode));
+            if (const char* v = std::getenv("JT_NODE_CACHE")) n = std::min<long>(n, std::max(0, std::atoi(v)));
+            S.nlnodes = (int)n;
+        }
     }
     S.ovf = nullptr;
     S.ovf_stride = 0;

@@ -14,6 +14,6 @@ EC="--scene assets/scenes/ecosys/ecosys.json --width 3840 --height 2160 --spp 8"
 for cfg in "$@"; do
   for sc in F2 B1 EC; do
     ( if [ "$cfg" != default ]; then IFS=','; for kv in $cfg; do export "$kv"; done; unset IFS; fi
-      scripts/gpu_step.sh 300 gpurun_out/$tag/bench_${sc}_$(echo $cfg | tr ',=' '_-').log python bench.py --no-cpu-baseline ${!sc} --steps 2 --warmup 1 ) || exit 1
+      scripts/gpu_step.sh 300 gpurun_out/$tag/bench_${sc}_$(echo $cfg | tr ',=/' '_-_').log python bench.py --no-cpu-baseline ${!sc} --steps 2 --warmup 1 ) || exit 1
   done
 done

@@ -1,16 +1,29 @@
-"""Summarise rocprofv3 --pmc csv passes: per-dispatch averages for the trace kernel."""
+"""Summarise rocprofv3 --pmc csv passes: per-dispatch averages for the trace kernel.
+
+usage: python scripts/pmc_summary.py <dir with p*/ passes> [kernel-name substring, default: the
+production (COUNT=0) instances, i.e. names containing "trace_kernel" and not ", 1, " as COUNT]"""
 import collections
 import csv
 import glob
 import sys
 
 root = sys.argv[1]
+want = sys.argv[2] if len(sys.argv) > 2 else None
+
+
+def match(name):
+    if want is not None:
+        return want in name
+    if "trace_kernel" not in name:
+        return False
+    targs = name[name.index("<") + 1:name.index(">")].split(",")
+    return len(targs) >= 4 and targs[3].strip() == "0"  # COUNT=0: the timed kernel, not the counting pass
 agg = collections.defaultdict(list)
 meta = {}
 for f in sorted(glob.glob(f"{root}/p*/p*_counter_collection.csv")):
     per = collections.defaultdict(float)
     for r in csv.DictReader(open(f)):
-        if "trace_kernel" not in r["Kernel_Name"]:
+        if not match(r["Kernel_Name"]):
             continue
         per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
         meta = {k: r[k] for k in ("Kernel_Name", "VGPR_Count", "SGPR_Count", "LDS_Block_Size", "Scratch_Size")}
