@@ -49,8 +49,9 @@ enum : int {
     FT_ENV = 16,   // environments (escaped rays, environment lights)
     FT_OPAC = 32,  // opacity < 1 possible (material opacity, color-texture or vertex-color alpha)
     FT_VOL = 64,   // refractive / subsurface / volumetric materials (the volume stack)
+    FT_XFORM = 128,  // instances whose inverse frame is not exactly the identity
     FT_NONE = 0,
-    FT_ALL = 127
+    FT_ALL = 255
 };
 struct alignas(16) DShape {
     int kind, blas_root, prim_base, idx_base;

@@ -410,16 +410,18 @@ __device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* 
 // test of its BLAS root are one step: the reference's instance visit pushes nothing but the
 // root (src/bvh.jl:345-351, 502-506), which is then the very next pop, so testing it in the same
 // step visits the same nodes in the same order.
-template <int RING, bool OVF, int COUNT, bool NCACHE>
+template <int RING, bool OVF, int COUNT, bool NCACHE, int F>
 __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
+    // without FT_XFORM every instance ray is the world ray: no transform, no space switch
+    constexpr bool XF = (F & FT_XFORM) != 0;
     const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
     unsigned type = e >> 30, idx = e & IDX_MASK;
     if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
         if (COUNT) cnt.instances++;
         const int4 ib = S.inst_blas[idx];  // blas_root, kind, identity, shape
-        if (ib.z) {
+        if (!XF || ib.z) {
             // inverse(identity) is exactly the identity: transform_ray returns the ray bit for bit
-            if (T.inst_space) world_ray(T);
+            if (XF && T.inst_space) world_ray(T);
         } else {
             const DInstTrav it = S.inst_trav[idx];
             const fr3 inv = frame_from(it.i0, it.i1, it.i2);
@@ -433,7 +435,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         T.cur_kind = ib.y;
         type = T_BLAS;
         idx = (unsigned)ib.x;
-    } else if (type == T_TLAS && T.inst_space) {
+    } else if (XF && type == T_TLAS && T.inst_space) {
         world_ray(T);  // back from an instance: TLAS nodes test the world ray
     }
     const bool blas = type == T_BLAS;
@@ -968,7 +970,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 // per-iteration vote and loop overhead)
 #pragma unroll
                 for (int k = 0; k < JT_NODE_REPEAT; k++)
-                    if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE>(S, T, stack, pixel, cnt);
+                    if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
             }
         }
 #if JT_STAMPS
@@ -1041,7 +1043,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 }
                 // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
                 // where most of the wave's lanes take part, rather than in a sparser traversal step
-                if (JT_FIRST_POP) node_step<RING, OVF, COUNT, NCACHE>(S, T, stack, pixel, cnt);
+#pragma unroll
+                for (int k = 0; k < JT_FIRST_POP; k++)
+                    if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
             }
 #if JT_STAMPS
             t_qb += __builtin_amdgcn_s_memtime() - s3;
@@ -1179,7 +1183,7 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
 // scenes with a 16-entry stack (cornellbox), and three masks for large HBM-mode scenes with the
 // ring + HBM overflow stack — textured, attributed meshes (bathroom1), plus environments
 // (ecosys), plus quads (features2).
-constexpr int FT_MESH = FT_TEX | FT_ATTR | FT_MAT | FT_OPAC;
+constexpr int FT_MESH = FT_TEX | FT_ATTR | FT_MAT | FT_OPAC | FT_XFORM;
 constexpr int FT_MESH_ENV = FT_MESH | FT_ENV;
 constexpr int FT_MESH_ENV_QUAD = FT_MESH_ENV | FT_QUAD;
 // the kernel mask a scene with feature bits `feat` runs with (the smallest compiled superset)
@@ -1613,6 +1617,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         bool ident = true;
         for (int q = 0; q < 12; q++) ident = ident && iv[q] == idm[q];
         iblas[k] = make_int4(d.blas_root, d.kind, ident ? 1 : 0, in.shape);
+        if (!ident) c->feat |= FT_XFORM;
         ishade[k] = DInstShade{f4(fv[0], fv[1], fv[2], fv[3]), f4(fv[4], fv[5], fv[6], fv[7]), f4(fv[8], fv[9], fv[10], fv[11]),
                                in.material, in.shape, scene->materials[in.material].type,
                                rot_identity(fv) ? 1 : 0};

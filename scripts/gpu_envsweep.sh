@@ -9,5 +9,5 @@ if [ -z "$NO_TESTS" ]; then
 fi
 for cfg in "$@"; do
   ( IFS=','; for kv in $cfg; do export "$kv"; done
-    scripts/gpu_step.sh 300 gpurun_out/$tag/bench_$(echo $cfg | tr ',=' '_-').log python bench.py --no-cpu-baseline ) || exit 1
+    scripts/gpu_step.sh 300 gpurun_out/$tag/bench_$(echo $cfg | tr ',=/' '_-_').log python bench.py --no-cpu-baseline ) || exit 1
 done
