@@ -18,9 +18,11 @@
 namespace jtd {
 
 // ------------------------------------------------------------------------------ layout in HBM
-// BVH node, 32 B = two 16-B loads: a = (bmin.xyz, start bits), b = (bmax.xyz, meta bits)
-// meta = num | axis << 16 | internal << 24. TLAS and all BLAS live in separate arrays;
-// BLAS `start` is a global node index (internal) or a global primitive-record slot (leaf).
+// BVH node, 32 B = two 16-B loads: a = (bmin.x, bmax.x, bmin.y, bmax.y), b = (bmin.z, bmax.z,
+// start bits, meta bits): each axis's slab planes are adjacent, so the slab test runs on packed
+// FP32 pairs (v_pk_add/v_pk_mul_f32). meta = num | axis << 16 | internal << 24. TLAS nodes come
+// first, then every BLAS; `start` is a global node index (internal) or a primitive-record slot
+// (BLAS leaf) or a tlas_prims index (TLAS leaf).
 struct alignas(16) DNode {
     float4 a, b;
 };
@@ -495,10 +497,14 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
 // separately, so the min/max chains below only ever see non-NaN values, where IEEE min/max
 // agree with Julia's (signed zeros cannot change `t0 <= t1`) and the order of the chain does
 // not matter.
+// a = (bmin.x, bmax.x, bmin.y, bmax.y), b = (bmin.z, bmax.z, ..) (DNode). Scalar on purpose:
+// packed-FP32 (v_pk_add/v_pk_mul_f32) forms of these products measured 1.5 % slower on gfx950
+// (the broadcast ray operands then occupy register pairs).
 __device__ __forceinline__ bool intersect_bbox(v3 o, v3 dinv, float tmin, float tmax, const float4& a,
                                                const float4& b) {
-    float mx = (a.x - o.x) * dinv.x, my = (a.y - o.y) * dinv.y, mz = (a.z - o.z) * dinv.z;
-    float Mx = (b.x - o.x) * dinv.x, My = (b.y - o.y) * dinv.y, Mz = (b.z - o.z) * dinv.z;
+    const float mx = (a.x - o.x) * dinv.x, Mx = (a.y - o.x) * dinv.x;
+    const float my = (a.z - o.y) * dinv.y, My = (a.w - o.y) * dinv.y;
+    const float mz = (b.x - o.z) * dinv.z, Mz = (b.y - o.z) * dinv.z;
     bool nan = __builtin_isnan(mx) | __builtin_isnan(my) | __builtin_isnan(mz) | __builtin_isnan(Mx) |
                __builtin_isnan(My) | __builtin_isnan(Mz);
     float t0 = vmax3(vmin(mx, Mx), vmin(my, My), vmax(vmin(mz, Mz), tmin));

@@ -330,22 +330,27 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
 // pairs: both tests are computed side by side (the record after the leaf's last one exists: the
 // array is padded), then accepted in order, the second against the tmax the first left. A
 // second pair runs in the same step when some lane's leaf has more than two left.
+// Triangle k of the current leaf and the next one come from one 80-B pair record (host layout:
+// the two triangles' components interleaved, 5 loads instead of 6 for two separate records).
+// k is 0 or 2.
 template <int F>
 __device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
-    const float4* r = S.prims + 3 * (T.prim + k);
-    const float4 a = r[0], b = r[1], c = r[2], a2 = r[3], b2 = r[4], c2 = r[5];
-    const PrimHit p1 = intersect_triangle_pre(T.lo, T.ld, ray_eps, xyz(a), xyz(b), xyz(c));
-    const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, xyz(a2), xyz(b2), xyz(c2));
+    const float4* r = S.prims + 5 * (T.prim + (k >> 1));
+    const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
+    const PrimHit p1 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.x, r0.z, r1.x), V3(r1.z, r2.x, r2.z),
+                                              V3(r3.x, r3.z, r4.x));
+    const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.y, r0.w, r1.y), V3(r1.w, r2.y, r2.w),
+                                              V3(r3.y, r3.w, r4.y));
     if (tri_hit_before(p1, T.tmax)) {
         T.h_inst = T.cur_inst;
-        T.h_elem = __float_as_int(a.w);
+        T.h_elem = __float_as_int(r4.z);
         T.h_u = p1.u;
         T.h_v = p1.v;
         T.tmax = p1.t;
     }
     if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax)) {
         T.h_inst = T.cur_inst;
-        T.h_elem = __float_as_int(a2.w);
+        T.h_elem = __float_as_int(r4.w);
         T.h_u = p2.u;
         T.h_v = p2.v;
         T.tmax = p2.t;
@@ -361,7 +366,7 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
         }
         const int n = T.nprim < 4 ? T.nprim : 4;
         if (COUNT) cnt.prims += n;
-        T.prim += n;
+        T.prim += 2;  // pair records (only read again when the leaf had more than four)
         T.nprim -= n;
         return;
     }
@@ -443,7 +448,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
     if (COUNT) cnt.nodes++;
     if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
     const unsigned meta = __float_as_uint(nd.b.w);
-    const int start = __float_as_int(nd.a.w);
+    const int start = __float_as_int(nd.b.z);
     const int num = (int)(meta & 0xffffu);
     if (meta >> 24) {  // internal: for d[axis] >= 0 push start, start+1 (start+1 pops first)
         const int axis = (int)((meta >> 16) & 0xffu);
@@ -1308,7 +1313,7 @@ bool rot_identity(const float* fv) {
 }
 DNode pack_node(const jt_bvh_node& n, int start) {
     unsigned meta = (unsigned)(uint16_t)n.num | ((unsigned)(uint8_t)n.axis << 16) | ((unsigned)(n.internal ? 1 : 0) << 24);
-    return DNode{f4(n.bmin[0], n.bmin[1], n.bmin[2], as_f(start)), f4(n.bmax[0], n.bmax[1], n.bmax[2], as_f(meta))};
+    return DNode{f4(n.bmin[0], n.bmax[0], n.bmin[1], n.bmax[1]), f4(n.bmin[2], n.bmax[2], as_f(start), as_f(meta))};
 }
 
 int check_tree(const jt_bvh_tree& t, int nprims_expected, const char* what) {
@@ -1519,10 +1524,10 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         const jt_bvh_tree& t = bvh->blas[s];
         DShape& d = shapes[s];
         d.kind = sh.ntriangles ? KIND_TRI : KIND_QUAD;
-        const int stride = d.kind == KIND_TRI ? 3 : 4;
+        const int stride = d.kind == KIND_TRI ? 5 : 4;
         d.blas_root = (int)tlas.size() + (int)blas.size();  // global index: TLAS nodes come first
-        // records are 3 (triangle) or 4 (quad) float4s: align the shape's first record to its
-        // stride so prim_base * stride addresses it exactly when shape kinds are mixed
+        // records are triangle pairs of 5 float4s or quads of 4: align the shape's first record to
+        // its stride so prim_base * stride addresses it exactly when shape kinds are mixed
         while (prims.size() % stride) prims.push_back(f4(0, 0, 0, 0));
         d.prim_base = (int)(prims.size() / stride);  // in records
         d.idx_base = (int)elems.size();
@@ -1570,32 +1575,62 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                 elems.push_back(make_int4(d.pos_base + sh.quads[4 * k], d.pos_base + sh.quads[4 * k + 1],
                                           d.pos_base + sh.quads[4 * k + 2], d.pos_base + sh.quads[4 * k + 3]));
         }
+        auto P3 = [&](int vi) { return f4(sh.positions[3 * vi], sh.positions[3 * vi + 1], sh.positions[3 * vi + 2], 0); };
+        if (d.kind == KIND_TRI) {
+            // Triangle-pair records, leaf by leaf (a leaf starts a record; an odd leaf's last
+            // record has a zero second triangle, never accepted: the leaf count masks it). The
+            // two triangles' components are interleaved so the pair test runs on packed FP32:
+            //   (p1x p1x' p1y p1y') (p1z p1z' e1x e1x') (e1y e1y' e1z e1z') (e2x e2x' e2y e2y')
+            //   (e2z e2z' el el'), edge1 = p2 - p1, edge2 = p3 - p1 (src/geometry.jl:208-209).
+            // The records hold the reference's floats for bvh.primitives[i], pre-gathered.
+            int pairs = 0;
+            for (int k = 0; k < t.nnodes; k++) {
+                const jt_bvh_node& n = t.nodes[k];
+                if (n.internal) {
+                    blas.push_back(pack_node(n, d.blas_root + n.start));
+                    continue;
+                }
+                blas.push_back(pack_node(n, d.prim_base + pairs));
+                for (int q = 0; q < n.num; q += 2) {
+                    float4 p[2], e1[2], e2[2];
+                    int el[2] = {-1, -1};
+                    for (int h = 0; h < 2; h++) {
+                        p[h] = e1[h] = e2[h] = f4(0, 0, 0, 0);
+                        if (q + h >= n.num) continue;
+                        el[h] = t.primitives[n.start + q + h];
+                        const int* v = &sh.triangles[3 * el[h]];
+                        const float4 a = P3(v[0]), b = P3(v[1]), cc = P3(v[2]);
+                        p[h] = a;
+                        e1[h] = f4(b.x - a.x, b.y - a.y, b.z - a.z, 0);
+                        e2[h] = f4(cc.x - a.x, cc.y - a.y, cc.z - a.z, 0);
+                    }
+                    prims.push_back(f4(p[0].x, p[1].x, p[0].y, p[1].y));
+                    prims.push_back(f4(p[0].z, p[1].z, e1[0].x, e1[1].x));
+                    prims.push_back(f4(e1[0].y, e1[1].y, e1[0].z, e1[1].z));
+                    prims.push_back(f4(e2[0].x, e2[1].x, e2[0].y, e2[1].y));
+                    prims.push_back(f4(e2[0].z, e2[1].z, as_f(el[0]), as_f(el[1])));
+                    pairs++;
+                }
+            }
+            continue;
+        }
         for (int k = 0; k < t.nnodes; k++) {
             const jt_bvh_node& n = t.nodes[k];
             blas.push_back(pack_node(n, n.internal ? d.blas_root + n.start : d.prim_base + n.start));
         }
-        // primitive records in BVH leaf order (the reference reads positions through
+        // quad records in BVH leaf order (the reference reads positions through
         // bvh.primitives[i]; the records hold the same floats, pre-gathered)
         for (int k = 0; k < t.nprimitives; k++) {
             const int el = t.primitives[k];
-            const int* v = d.kind == KIND_TRI ? &sh.triangles[3 * el] : &sh.quads[4 * el];
-            auto P3 = [&](int vi) { return f4(sh.positions[3 * vi], sh.positions[3 * vi + 1], sh.positions[3 * vi + 2], 0); };
-            float4 a = P3(v[0]), b = P3(v[1]), cc = P3(v[2]);
+            const int* v = &sh.quads[4 * el];
+            float4 a = P3(v[0]), b = P3(v[1]), cc = P3(v[2]), dd = P3(v[3]);
             a.w = as_f(el);
+            const bool degenerate = cc.x == dd.x && cc.y == dd.y && cc.z == dd.z;  // p3 == p4
+            dd.w = degenerate ? 1.0f : 0.0f;
             prims.push_back(a);
-            if (d.kind == KIND_TRI) {  // edge1 = p2 - p1, edge2 = p3 - p1 (src/geometry.jl:208-209)
-                prims.push_back(f4(b.x - a.x, b.y - a.y, b.z - a.z, 0));
-                prims.push_back(f4(cc.x - a.x, cc.y - a.y, cc.z - a.z, 0));
-            } else {
-                prims.push_back(b);
-                prims.push_back(cc);
-            }
-            if (d.kind == KIND_QUAD) {
-                float4 dd = P3(v[3]);
-                const bool degenerate = cc.x == dd.x && cc.y == dd.y && cc.z == dd.z;  // p3 == p4
-                dd.w = degenerate ? 1.0f : 0.0f;
-                prims.push_back(dd);
-            }
+            prims.push_back(b);
+            prims.push_back(cc);
+            prims.push_back(dd);
         }
     }
     std::vector<DInstTrav> itrav(scene->ninstances);
