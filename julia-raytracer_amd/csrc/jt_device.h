@@ -19,10 +19,10 @@ namespace jtd {
 
 // ------------------------------------------------------------------------------ layout in HBM
 // BVH node, 32 B = two 16-B loads: a = (bmin.x, bmax.x, bmin.y, bmax.y), b = (bmin.z, bmax.z,
-// start bits, meta bits): each axis's slab planes are adjacent, so the slab test runs on packed
-// FP32 pairs (v_pk_add/v_pk_mul_f32). meta = num | axis << 16 | internal << 24. TLAS nodes come
-// first, then every BLAS; `start` is a global node index (internal) or a primitive-record slot
-// (BLAS leaf) or a tlas_prims index (TLAS leaf).
+// start bits, meta bits), each axis's slab planes side by side. meta = num | axis << 16 |
+// internal << 24. TLAS nodes come first (breadth-first), then every BLAS; `start` is a global
+// node index (internal), a triangle-pair / quad record slot (BLAS leaf) or a tlas_prims index
+// (TLAS leaf).
 struct alignas(16) DNode {
     float4 a, b;
 };
@@ -90,7 +90,8 @@ struct alignas(16) DLight {
 struct DScene {
     const DNode* nodes;      // TLAS nodes, then every BLAS (global node indices)
     const int* tlas_prims;  // instance ids in leaf order
-    const float4* prims;  // triangle: 3 float4 (p1|elem, p2-p1, p3-p1); quad: 4 float4 (p4.w = p3==p4)
+    const float4* prims;  // triangle pair: 5 float4 (p1, p2-p1, p3-p1 of two triangles interleaved,
+                          // then both element ids); quad: 4 float4 (p1|elem, p2, p3, p4|p3==p4)
     const DInstTrav* inst_trav;
     const int4* inst_blas;  // per instance: blas_root, kind, identity-transform flag, shape
     const DInstShade* inst_shade;

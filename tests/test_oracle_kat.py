@@ -57,10 +57,36 @@ def test_fresnel_dielectric(oracle):
     assert fresnel(oracle, 1 / 1.5, (0, 0, 1), (0, float(np.sqrt(1 - c * c)), float(c))) == 1.0  # TIR
 
 
+def _mix64(z):
+    m = (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def _pcg32_floats(seed, pixel, sample, n):
+    """Independent restatement of the build's RNG: PCG32 (XSH-RR) keyed by
+    SplitMix64 finalisers of (seed, pixel, sample); rand1f = (x >> 8) * 2^-24."""
+    m64, mult = (1 << 64) - 1, 6364136223846793005
+    key = _mix64(seed ^ _mix64((pixel << 32) | sample))
+    inc = ((_mix64(key ^ 0xDA3E39CB94B95BDB) << 1) | 1) & m64
+    state = ((inc + key) * mult + inc) & m64
+    out = []
+    for _ in range(n):
+        old = state
+        state = (old * mult + inc) & m64
+        xs = (((old >> 18) ^ old) >> 27) & 0xFFFFFFFF
+        rot = old >> 59
+        x = ((xs >> rot) | (xs << ((32 - rot) & 31))) & 0xFFFFFFFF
+        out.append(np.float32(x >> 8) * np.float32(2.0**-24))
+    return np.array(out, np.float32)
+
+
 def test_rng_stream(oracle):
     out = (C.c_float * 4096)()
     oracle.lib.or_rng_first(0x5EED, 17, 3, 4096, out)
     v = np.array(out)
+    np.testing.assert_array_equal(v.astype(np.float32), _pcg32_floats(0x5EED, 17, 3, 4096))
     assert np.all((v >= 0) & (v < 1))
     assert np.all(v * 2**24 == np.floor(v * 2**24))  # 24-bit resolution like rand(Float32)
     assert abs(v.mean() - 0.5) < 0.02
