@@ -101,15 +101,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (not used by the driver): JT_BENCH_BACKEND=gloo reduces through host
+    # memory, JT_BENCH_DEVICE pins every rank to one GPU — N ranks on a one-GPU box
+    backend = os.environ.get("JT_BENCH_BACKEND", "nccl")
+    dev = int(os.environ.get("JT_BENCH_DEVICE", str(local_rank)))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     from jtrace import abi, sceneio, trace
     from jtrace.cli import Params
@@ -117,7 +124,7 @@ def main():
     scene = sceneio.load_scene(args.scene, missing="drop")  # configs 3-5: the checkout lacks a few files
     sa = abi.SceneABI(scene)
     params = Params(scene=args.scene, samples=args.spp, sampler=2 if args.sampler == "naive" else 1,
-                    width=args.width, height=args.height, device=local_rank, batch=args.spp)
+                    width=args.width, height=args.height, device=dev, batch=args.spp)
     jp = abi.make_params(params, 0)
     bvh = trace.make_scene_bvh(sa, False, lib)
     lights = trace.make_trace_lights(sa, lib)
@@ -133,13 +140,13 @@ def main():
         class _CAI:  # view the library's running-mean buffer as a torch tensor (no copy)
             __cuda_array_interface__ = {"shape": (H * W * 4,), "typestr": "<f4",
                                         "data": (buf.image, False), "version": 3}
-        img_t = torch.as_tensor(_CAI(), device=f"cuda:{local_rank}")
+        img_t = torch.as_tensor(_CAI(), device=f"cuda:{dev}")
 
     def step():
         state.reset()
         state.trace_range(s0, s1)  # returns when the launch has finished (HIP event sync)
         if world > 1:  # the path's one exchange: sum of sample-weighted shard means (RCCL)
-            reduce_running_means(img_t, s1 - s0, S, dist, dst=0)
+            reduce_running_means(img_t if backend == "nccl" else img_t.cpu(), s1 - s0, S, dist, dst=0)
             # the reduce reads the library's buffer on torch's stream: finish it before the next
             # step's jt_reset clears that buffer on the library's stream
             torch.cuda.synchronize()
@@ -174,7 +181,7 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=f"cuda:{local_rank}")
+    t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
     if dist is not None:
         tmax = t.clone()
         dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)

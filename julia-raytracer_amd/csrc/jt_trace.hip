@@ -36,6 +36,9 @@
 #ifndef JT_FIRST_POP
 #define JT_FIRST_POP 1
 #endif
+#ifndef JT_FUSED
+#define JT_FUSED 0
+#endif
 
 using namespace jtd;
 
@@ -967,7 +970,13 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             n_trav++;
             if (np >= nn) { steps_p++; lanes_p += np; } else { steps_n++; lanes_n += nn; }
 #endif
-            if (np >= nn) {
+            if (JT_FUSED) {
+                // both step kinds every iteration, each on the lanes that want it
+                if (np > 0 && T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+#pragma unroll
+                for (int k = 0; k < JT_NODE_REPEAT; k++)
+                    if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+            } else if (np >= nn) {
                 if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
             } else {
                 // JT_NODE_REPEAT pops per node iteration: a lane whose next step is again a
