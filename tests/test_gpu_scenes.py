@@ -163,3 +163,29 @@ def test_stack_overflow_to_hbm_is_exact(gpu, abi, lib, monkeypatch, name, ring):
         assert np.array_equal(a, b)
     for k in ("rays", "light_queries", "nodes", "instances", "prims", "shades"):
         assert outs[0][2][k] == outs[1][2][k], k
+
+
+@pytest.mark.parametrize("name,mask", [("bathroom1", ",171> "), ("ecosys", ",187> "), ("features2", ",191> ")])
+def test_mesh_specialisations_bitwise_equal(gpu, abi, lib, monkeypatch, name, mask):
+    """Configs 3-5 run the large-scene specialisations (FT_MESH, FT_MESH_ENV, FT_MESH_ENV_QUAD,
+    HBM mode with the child pre-test and the LDS copy of the TLAS top): the general FT_ALL kernel
+    (JT_FEATURES=all) must give the same image, AOVs and traversal counters, bit for bit."""
+    from jtrace import trace
+    sa = scene_abi(name)
+    p = make_params(abi, resolution=96, samples=2)
+    bvh = trace.make_scene_bvh(sa, False, lib)
+    lights = trace.make_trace_lights(sa, lib)
+    outs = []
+    for feat in ("auto", "all"):
+        monkeypatch.setenv("JT_FEATURES", feat)
+        st = trace.make_trace_state(sa, bvh, lights, p, lib)
+        st.set_counters(1)
+        st.trace_range(0, 2)
+        outs.append((st.get_image(), st.get_aovs(), st.counters(), st.describe()))
+        st.close()
+    assert mask in outs[0][3] and ",255> " in outs[1][3], (outs[0][3], outs[1][3])
+    assert np.array_equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert np.array_equal(a, b)
+    for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades"):
+        assert outs[0][2][k] == outs[1][2][k], k
