@@ -251,13 +251,16 @@ __device__ __forceinline__ v3 eval_environment(const DScene& S, v3 direction) {
 }
 
 // ============================================================================ traversal (src/bvh.jl)
-// Unified per-lane stack in LDS, entry = type << 30 | index. Layout stack[k * BLOCK + lane]:
+// Unified per-lane stack in LDS, entry = type << 30 | snap << 24 | index (24 bits; jt_create
+// checks the scene fits). snap (HBM mode): the query's hit count when a pre-tested child was
+// pushed (SNAP_NONE: not pre-tested). Layout stack[k * BLOCK + lane]:
 // every lane owns one bank (conflict-free ds_read/write_b32 whatever the per-lane depth).
 // The LDS part is a ring of RING entries; when a scene's bound exceeds it (OVF), the oldest
 // entries spill to a per-pixel HBM area and come back one at a time when popped.
 constexpr int BLOCK = 256;
 constexpr unsigned T_TLAS = 0u, T_INST = 1u, T_BLAS = 2u;
-constexpr unsigned IDX_MASK = (1u << 30) - 1;
+constexpr unsigned IDX_MASK = (1u << 24) - 1;
+constexpr unsigned SNAP_NONE = 63u << 24;
 
 struct Hit {
     int inst, elem;
@@ -288,6 +291,7 @@ struct Trav {
     int prim, nprim;   // leaf cursor: next primitive record, primitives left
     int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
     float h_u, h_v;
+    int nh;              // hits accepted so far (every tmax change), saturating at 63
 };
 
 __device__ __forceinline__ int neg_mask(v3 d) { return (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0); }
@@ -314,6 +318,7 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     T.ld = d;
     T.ldinv = T.wdinv;
     T.tmax = __builtin_inff();
+    T.nh = 0;
     T.h_inst = -1;
     T.h_elem = -1;
     T.h_u = 0;
@@ -345,6 +350,7 @@ __device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
     const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.y, r0.w, r1.y), V3(r1.w, r2.y, r2.w),
                                               V3(r3.y, r3.w, r4.y));
     if (tri_hit_before(p1, T.tmax)) {
+        T.nh += T.nh < 63 ? 1 : 0;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.z);
         T.h_u = p1.u;
@@ -352,6 +358,7 @@ __device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
         T.tmax = p1.t;
     }
     if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax)) {
+        T.nh += T.nh < 63 ? 1 : 0;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.w);
         T.h_u = p2.u;
@@ -378,6 +385,7 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     const float4 a = r[0], b = r[1], c = r[2], d = r[3];
     const PrimHit p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
     if (p.hit) {
+        T.nh += T.nh < 63 ? 1 : 0;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(a.w);
         T.h_u = p.u;
@@ -447,16 +455,26 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         world_ray(T);  // back from an instance: TLAS nodes test the world ray
     }
     const bool blas = type == T_BLAS;
-    const DNode nd = (NCACHE && (int)idx < S.nlnodes) ? S.lnodes[idx] : S.nodes[idx];
     if (COUNT) cnt.nodes++;
-    if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
-    const unsigned meta = __float_as_uint(nd.b.w);
-    const int start = __float_as_int(nd.b.z);
+    // HBM mode: a child pre-tested at its parent with the tmax it still has (no hit since: its
+    // snapshot equals the hit count) passes this pop's box test too — same ray, same box, same
+    // tmax — so only its start/meta half is loaded
+    const unsigned snap = (e >> 24) & 63u;
+    float4 nb;
+    if (NCACHE && snap != 63u && snap == (unsigned)T.nh) {
+        nb = ((int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
+    } else {
+        const DNode nd = (NCACHE && (int)idx < S.nlnodes) ? S.lnodes[idx] : S.nodes[idx];
+        if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
+        nb = nd.b;
+    }
+    const unsigned meta = __float_as_uint(nb.w);
+    const int start = __float_as_int(nb.z);
     const int num = (int)(meta & 0xffffu);
     if (meta >> 24) {  // internal: for d[axis] >= 0 push start, start+1 (start+1 pops first)
         const int axis = (int)((meta >> 16) & 0xffu);
         const bool neg = (T.negmask >> axis) & 1;  // d[axis] < 0
-        const unsigned tag = type << 30;
+        const unsigned tag = type << 30 | SNAP_NONE;
         const unsigned c_far = (unsigned)(neg ? start + 1 : start), c_near = (unsigned)(neg ? start : start + 1);
         if (JT_CHILD_PRETEST && NCACHE) {
             // HBM mode: test both children (one 64-B pair) when their parent is visited. A child
@@ -470,15 +488,16 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             const bool k0 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n0.a, n0.b);
             const bool k1 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n1.a, n1.b);
             if (COUNT) cnt.nodes += (k0 ? 0 : 1) + (k1 ? 0 : 1);
-            if (k0) st_push<RING, OVF>(S, T, stack, pixel, tag | c_far);
-            if (k1) st_push<RING, OVF>(S, T, stack, pixel, tag | c_near);
+            const unsigned ptag = type << 30 | (unsigned)T.nh << 24;  // pre-tested at hit count nh
+            if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_far);
+            if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_near);
         } else {
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_far);
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_near);
         }
     } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
         for (int k = num - 1; k >= 0; k--)
-            st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | (unsigned)S.tlas_prims[start + k]);
+            st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | SNAP_NONE | (unsigned)S.tlas_prims[start + k]);
     } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
@@ -940,7 +959,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     if (alive) {
         start_path(P, i, j, pixel, sample, st);
         cnt.rays++;
-        query_begin(T, st.o, st.d, T_TLAS << 30, stack);
+        query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
     }
     for (;;) {
 #if JT_STAMPS
@@ -972,10 +991,10 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                             st.phase = PH_FINISH;
                         } else if (st.phase == PH_LIGHT) {
                             cnt.light_queries++;
-                            query_begin(T, st.lq, st.d, (T_INST << 30) | (unsigned)S.lights[st.li].instance, stack);
+                            query_begin(T, st.lq, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
                         } else {
                             cnt.rays++;
-                            query_begin(T, st.o, st.d, T_TLAS << 30, stack);
+                            query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
                         }
                     }
                     continue;
@@ -1061,10 +1080,10 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (alive) {
                 if (SAMPLER == 1 && st.phase == PH_LIGHT) {
                     cnt.light_queries++;
-                    query_begin(T, st.lq, st.d, (T_INST << 30) | (unsigned)S.lights[st.li].instance, stack);
+                    query_begin(T, st.lq, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
                 } else {
                     cnt.rays++;
-                    query_begin(T, st.o, st.d, T_TLAS << 30, stack);
+                    query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
                 }
                 // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
                 // where most of the wave's lanes take part, rather than in a sparser traversal step
@@ -1767,6 +1786,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     for (int q = 0; q < 4; q++) prims.push_back(f4(0, 0, 0, 0));
     std::vector<DNode> nodes(tlas);
     nodes.insert(nodes.end(), blas.begin(), blas.end());
+    // traversal stack entries carry a 24-bit node / instance index (IDX_MASK)
+    if (nodes.size() > IDX_MASK || (size_t)scene->ninstances > IDX_MASK)
+        return bail(jt::fail(JT_ERR_UNSUPPORTED, "scene exceeds 2^24 BVH nodes or instances"));
     if ((st = upload(c, nodes, &S.nodes)) || (st = upload(c, tlas_prims, &S.tlas_prims)) || (st = upload(c, prims, &S.prims)) ||
         (st = upload(c, itrav, &S.inst_trav)) || (st = upload(c, iblas, &S.inst_blas)) || (st = upload(c, ishade, &S.inst_shade)) ||
         (st = upload(c, shapes, &S.shapes)) || (st = upload(c, pos, &S.pos)) || (st = upload(c, nrm, &S.nrm)) ||
