@@ -238,3 +238,42 @@ def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sa
             assert np.array_equal(a, b)
         for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades"):
             assert outs[0][2][k] == o[2][k], k
+
+
+def test_device_buffer_view_is_the_running_mean(gpu, abi, lib, cornell_abi):
+    """bench.py's multi-GPU reduce reads the library's running-mean image in place through
+    __cuda_array_interface__ (jt_get_device_buffers): that view must be exactly jt_get_image, and
+    the sample-weighted reduce of jtrace.parallel over a world of one rank must give it back."""
+    torch = pytest.importorskip("torch")
+    from jtrace import trace
+    from jtrace.parallel import reduce_running_means
+    bvh = trace.make_scene_bvh(cornell_abi, False, lib)
+    lights = trace.make_trace_lights(cornell_abi, lib)
+    st = trace.make_trace_state(cornell_abi, bvh, lights, make_params(abi, resolution=48, samples=3), lib)
+    st.trace_range(0, 3)
+    buf = st.device_buffers()
+    H, W = st.height, st.width
+
+    class _CAI:
+        __cuda_array_interface__ = {"shape": (H * W * 4,), "typestr": "<f4", "data": (buf.image, False), "version": 3}
+
+    dev = torch.as_tensor(_CAI(), device="cuda:0")
+    torch.cuda.synchronize()
+    host = st.get_image().reshape(-1)
+    np.testing.assert_array_equal(dev.cpu().numpy(), host)
+
+    class _OneRank:  # torch.distributed stand-in for a world of one rank: reduce is the identity
+        class ReduceOp:
+            SUM = None
+
+        @staticmethod
+        def reduce(t, dst, op):
+            return None
+
+        @staticmethod
+        def get_rank():
+            return 0
+
+    out = reduce_running_means(dev, 3, 3, _OneRank, dst=0)
+    np.testing.assert_allclose(out.cpu().numpy(), host, rtol=1e-6, atol=0)
+    st.close()
