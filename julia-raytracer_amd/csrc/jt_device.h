@@ -131,6 +131,7 @@ struct DScene {
     int* ovf;
     int ovf_stride;
     int ring;  // entries of the LDS ring in use (a power of two <= the kernel's RING)
+    int stack_need;  // stack bound of the scene: LDS-mode kernels without overflow allocate this many
     int o_nodes, o_tlas_prims, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
     int o_pos, o_nrm, o_tc, o_col, o_elems, o_materials, o_lights, o_cdf, o_enrm, o_enrm_id;
 };

@@ -1138,14 +1138,22 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     }
 }
 
-// Occupancy request (waves per SIMD); JT_WAVES=0 leaves it to the compiler.
+// Occupancy request (waves per SIMD); JT_WAVES=0 leaves it to the compiler. The LDS-mode
+// FT_NONE kernel (cornellbox: 96 VGPRs, LDS for 5 workgroups per CU with the stack sized to the
+// scene) asks for JT_WAVES_NONE: measured +4 % over 4 waves with its wait_lanes of 56.
 #ifndef JT_WAVES
 #define JT_WAVES 0
 #endif
+#ifndef JT_WAVES_NONE
+#define JT_WAVES_NONE 5
+#endif
 #if JT_WAVES > 0
 #define JT_WAVES_PER_EU __attribute__((amdgpu_waves_per_eu(JT_WAVES, JT_WAVES)))
+#define JT_WAVES_PER_EU_F(F) \
+    __attribute__((amdgpu_waves_per_eu((F) == FT_NONE ? JT_WAVES_NONE : JT_WAVES, (F) == FT_NONE ? JT_WAVES_NONE : JT_WAVES)))
 #else
 #define JT_WAVES_PER_EU
+#define JT_WAVES_PER_EU_F(F)
 #endif
 
 // HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS. The
@@ -1168,9 +1176,9 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, 
 // instance, primitive and shading record is then a ds_read instead of a vector-memory load
 // through the TA/TD path (the measured limiter of the HBM-mode kernel).
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
-__global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
+__global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     extern __shared__ uint4 dyn_lds[];
-    uint4* blob = dyn_lds + (RING * BLOCK) / 4;
+    uint4* blob = dyn_lds + ((OVF ? RING : S.stack_need) * BLOCK) / 4;  // the stack takes the first entries
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
     DScene L = S;
@@ -1205,7 +1213,7 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
     hipError_t e;
     if constexpr (LDSK) {
         if (S.blob_n16 > 0) {
-        const size_t lds = (size_t)RING * BLOCK * 4 + (size_t)S.blob_n16 * 16;
+        const size_t lds = (size_t)(OVF ? RING : S.stack_need) * BLOCK * 4 + (size_t)S.blob_n16 * 16;
         const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>;
         if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
@@ -1835,11 +1843,14 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         // with JT_LDS_SCENE=0 (off) or a byte budget for the blob.
         size_t budget = 48 * 1024;
         if (const char* v = std::getenv("JT_LDS_SCENE")) budget = (size_t)std::atoll(v);
-        const int stack_entries = c->stack <= 16 ? 16 : c->ring;
-        const size_t base_bytes = (size_t)stack_entries * 256 * 4 + (size_t)ACC_SLOTS * BLOCK * 4;
+        // HBM mode's stack is the kernel's static ring (16 or 32 entries); LDS mode's, without
+        // overflow, just the scene's bound
+        const size_t acc_bytes = (size_t)ACC_SLOTS * BLOCK * 4;
+        const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 4 + acc_bytes;
+        const size_t lds_base = (size_t)(c->stack <= 16 ? c->stack : c->ring) * BLOCK * 4 + acc_bytes;
         const size_t bytes = blob.size() * 16;
         const size_t lds_cu = 160 * 1024;
-        const size_t wg_hbm = std::min<size_t>(4, lds_cu / base_bytes), wg_lds = lds_cu / (base_bytes + bytes);
+        const size_t wg_hbm = std::min<size_t>(4, lds_cu / base_bytes), wg_lds = lds_cu / (lds_base + bytes);
         S.blob = nullptr;
         S.blob_n16 = 0;
         if (bytes <= budget && wg_lds >= wg_hbm) {
@@ -1862,6 +1873,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     S.ovf = nullptr;
     S.ovf_stride = 0;
     S.ring = c->ring;
+    S.stack_need = c->stack;
     // JT_LDS_RING (tests only): use fewer ring entries than allocated, to exercise the overflow
     if (const char* r = std::getenv("JT_LDS_RING")) {
         int v = std::atoi(r);
@@ -1911,7 +1923,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     // light-hit steps in the traversal phase (they take the light queries out of the phases)
     c->kmask = kernel_mask(c->feat, c->stack, c->ring, c->lds_scene_bytes > 0);
     const bool lstep = c->sampler != JT_SAMPLER_NAIVE && !(c->kmask & FT_ENV);  // LSTEP in trace_body
-    P.wait_lanes = lstep ? 48 : 40;
+    P.wait_lanes = lstep ? (c->kmask == FT_NONE && c->lds_scene_bytes ? 56 : 48) : 40;  // 5-wave FT_NONE: 56
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
     P.light_lanes = 2;
     if (const char* ll = std::getenv("JT_LIGHT_LANES")) P.light_lanes = std::max(1, std::min(65, std::atoi(ll)));
