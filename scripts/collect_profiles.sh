@@ -5,8 +5,7 @@ O=gpurun_out/final
 R=${ROUND:-r01}
 grep '^{' $O/bench.log > profiles/${R}_bench.log
 cp $O/kt/kt_kernel_stats.csv profiles/${R}_kernel_stats.csv
-K=$(python3 -c "import json;d=json.loads(open('profiles/${R}_bench.log').readline());k=d['roofline']['kernel'];print(k.replace(',', ', '))")
-python3 scripts/pmc_traffic.py $O/fetch $O/write "$K" "cornellbox path 1280x720 256 samples/launch" profiles/${R}_traffic.json
+cp $O/traffic.json profiles/${R}_traffic.json
 mkdir -p profiles/${R}_pmc profiles/${R}_scenes
 cp $O/pmc/cb_summary.txt profiles/${R}_pmc/cornellbox_lds_64spp.txt
 cp $O/pmc/b1_summary.txt profiles/${R}_pmc/bathroom1_hbm_1920x1080_16spp.txt
