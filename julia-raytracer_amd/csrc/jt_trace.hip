@@ -643,20 +643,32 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
 // its pixel for all its samples): acc[k * BLOCK], k = 0..3 image rgba, 4..6 albedo, 7..9
 // normal, 10 hit count of this launch (int). Loaded from / stored to HBM once per launch; the
 // per-sample lerps are the same float operations as a read-modify-write of the HBM buffers.
-constexpr int ACC_SLOTS = 11;
+// JT_LANE_LDS: 11 the lane's current sample (int), 12 its running-mean weight 1/(n+1) — per-sample
+// state parked in LDS instead of registers kept live (and spilled) across the traversal loop.
+#ifndef JT_LANE_LDS
+#define JT_LANE_LDS 1
+#endif
+// Not in the FT_NONE kernels: cornellbox's LDS-mode kernel then no longer fits 5 workgroups per
+// CU (-9 %); the mesh kernels gain (features2 +7 %, bathroom1 +1 %, ecosys +0.6 %).
+__host__ __device__ constexpr bool lane_lds(int F) { return JT_LANE_LDS && F != FT_NONE; }
+constexpr int ACC_SLOTS = JT_LANE_LDS ? 13 : 11;  // the host sizes LDS for the larger layout
 struct Aov {
     float* acc;
-    float w;
+    float w_;  // !lane_lds(F)
+    template <int F>
+    __device__ __forceinline__ float w() const { return lane_lds(F) ? acc[12 * BLOCK] : w_; }
 };
+template <int F>
 __device__ __forceinline__ void aov_update(const Aov& a, v3 ta, v3 tn) {
-    const float omw = 1 - a.w;
+    const float aw = a.w<F>();
+    const float omw = 1 - aw;
     float* p = a.acc;
-    p[4 * BLOCK] = p[4 * BLOCK] * omw + ta.x * a.w;
-    p[5 * BLOCK] = p[5 * BLOCK] * omw + ta.y * a.w;
-    p[6 * BLOCK] = p[6 * BLOCK] * omw + ta.z * a.w;
-    p[7 * BLOCK] = p[7 * BLOCK] * omw + tn.x * a.w;
-    p[8 * BLOCK] = p[8 * BLOCK] * omw + tn.y * a.w;
-    p[9 * BLOCK] = p[9 * BLOCK] * omw + tn.z * a.w;
+    p[4 * BLOCK] = p[4 * BLOCK] * omw + ta.x * aw;
+    p[5 * BLOCK] = p[5 * BLOCK] * omw + ta.y * aw;
+    p[6 * BLOCK] = p[6 * BLOCK] * omw + ta.z * aw;
+    p[7 * BLOCK] = p[7 * BLOCK] * omw + tn.x * aw;
+    p[8 * BLOCK] = p[8 * BLOCK] * omw + tn.y * aw;
+    p[9 * BLOCK] = p[9 * BLOCK] * omw + tn.z * aw;
 }
 
 template <int F>
@@ -694,7 +706,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
         }
         if (st.bounce == 0) {
             st.flags |= F_HIT;
-            aov_update(aov, sh.mat.color, sh.normal);
+            aov_update<F>(aov, sh.mat.color, sh.normal);
         }
         st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
         v3 incoming;
@@ -778,7 +790,7 @@ __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Pat
     }
     if (st.bounce == 0) {
         st.flags |= F_HIT;
-        aov_update(aov, sh.mat.color, sh.normal);
+        aov_update<F>(aov, sh.mat.color, sh.normal);
     }
     st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
     v3 incoming, f;
@@ -897,6 +909,13 @@ __device__ __forceinline__ void publish_tile(const DAccum& A, int t, int c) {
     if ((threadIdx.x & 63) == 0) __hip_atomic_store(A.tile_done + t, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// lane id (0..63) recomputed where it is used: an asm the compiler cannot merge with an earlier one
+__device__ __forceinline__ int opaque_lane_id() {
+    unsigned l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return (int)l;
+}
+
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
 // mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
@@ -905,7 +924,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                                            int* stack) {
     const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    __shared__ float acc_lds[ACC_SLOTS * BLOCK];
+    constexpr bool LL = lane_lds(F);
+    __shared__ float acc_lds[(LL ? 13 : 11) * BLOCK];
     float* acc = acc_lds + threadIdx.x;
 #if JT_STAMPS
     unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
@@ -931,8 +951,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     const int i = (ut % tiles_x) * 8 + (lane & 7);
     const int j = (ut / tiles_x) * 8 + (lane >> 3);
     const int cs0 = s_begin + uc * P.chunk, cs1 = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
-    const int pixel = j * P.width + i;
-    const bool in_image = i < P.width && j < P.height;
+    int pixel = j * P.width + i;
+    bool in_image = i < P.width && j < P.height;
     bool alive = in_image;
     int sample = cs0;
     if (in_image) {
@@ -949,7 +969,16 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         acc[9 * BLOCK] = nr.z;
         reinterpret_cast<int*>(acc)[10 * BLOCK] = 0;
     }
-    Aov aov{acc, 1.0f / (float)(sample - P.first + 1)};
+    int* const acc_i = reinterpret_cast<int*>(acc);
+    Aov aov{acc, 0.0f};
+    if (LL) {
+        if (in_image) {
+            acc_i[11 * BLOCK] = sample;
+            acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+        }
+    } else {
+        aov.w_ = 1.0f / (float)(sample - P.first + 1);
+    }
     Path st;
     Trav T;
     // lane states, from the stack cursor alone: sp < 0 finished (no samples left), nprim > 0 or
@@ -1053,24 +1082,40 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 if (!all_finite(radiance)) radiance = V3(0, 0, 0);
                 const float mr = max3(radiance);
                 if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
-                const float w = aov.w;
+                const float w = aov.w<F>();
                 const float omw = 1 - w;
                 const bool hit = st.flags & F_HIT;
                 const bool env = !hit && !P.envhidden && S.nenvs != 0;
                 const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
                 // no bounce-0 surface was accepted: st.d is still the camera ray direction
-                if (!hit) aov_update(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
+                if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
                 acc[0] = acc[0] * omw + target.x * w;
                 acc[BLOCK] = acc[BLOCK] * omw + target.y * w;
                 acc[2 * BLOCK] = acc[2 * BLOCK] * omw + target.z * w;
                 acc[3 * BLOCK] = acc[3 * BLOCK] * omw + target.w * w;
                 if (hit || env) reinterpret_cast<int*>(acc)[10 * BLOCK] += 1;
+                if constexpr (LL) {
+                // the pixel from the unit's wave-uniform tile and a lane id the compiler cannot
+                // reuse from the top of the unit, so i / j do not stay live across the loop
+                const int sample = acc_i[11 * BLOCK] + 1;
+                if (sample >= cs1) {
+                    alive = false;
+                    T.sp = -1;
+                } else {
+                    acc_i[11 * BLOCK] = sample;
+                    acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+                    const int lx = opaque_lane_id();
+                    const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
+                    start_path(P, i2, j2, j2 * P.width + i2, sample, st);
+                }
+                } else {
                 if (++sample >= cs1) {
                     alive = false;
                     T.sp = -1;
                 } else {
-                    aov.w = 1.0f / (float)(sample - P.first + 1);
+                    aov.w_ = 1.0f / (float)(sample - P.first + 1);
                     start_path(P, i, j, pixel, sample, st);
+                }
                 }
             }
 #if JT_STAMPS
@@ -1099,6 +1144,12 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         t_shade += __builtin_amdgcn_s_memtime() - t1;
 #endif
         if (__ballot(T.sp >= 0) == 0) break;
+    }
+    if constexpr (LL) {
+        const int lx = opaque_lane_id();
+        const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
+        pixel = j2 * P.width + i2;
+        in_image = i2 < P.width && j2 < P.height;
     }
     if (in_image) {
         A.image[pixel] = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);
