@@ -1974,7 +1974,11 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     // light-hit steps in the traversal phase (they take the light queries out of the phases)
     c->kmask = kernel_mask(c->feat, c->stack, c->ring, c->lds_scene_bytes > 0);
     const bool lstep = c->sampler != JT_SAMPLER_NAIVE && !(c->kmask & FT_ENV);  // LSTEP in trace_body
-    P.wait_lanes = lstep ? (c->kmask == FT_NONE && c->lds_scene_bytes ? 56 : 48) : 40;  // 5-wave FT_NONE: 56
+    // deep BVHs (stack bound > 32: bathroom1, ecosys) shade sooner: their lanes finish queries far
+    // apart, so waiting for many leaves the wave idle (measured: bathroom1 48 -> 32 +5 %, ecosys
+    // 40 -> 16 +15 %; features2 and cornellbox keep 40 / 56)
+    const bool deep = c->stack > 32;
+    P.wait_lanes = lstep ? (c->kmask == FT_NONE && c->lds_scene_bytes ? 56 : deep ? 32 : 48) : deep ? 16 : 40;
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
     P.light_lanes = 2;
     if (const char* ll = std::getenv("JT_LIGHT_LANES")) P.light_lanes = std::max(1, std::min(65, std::atoi(ll)));
