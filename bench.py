@@ -24,8 +24,14 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "julia-raytracer_amd"))
 
-METRIC = "Mrays/s + wall-clock render time, cornellbox 1280×720×256spp"
+METRIC_BASE = "Mrays/s + wall-clock render time"  # BASELINE.json metric; the workload is appended
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def metric_name(scene: str, sampler: str, W: int, H: int, S: int) -> str:
+    """BASELINE.json's metric string for this workload ("..., cornellbox 1280×720×256spp"); the
+    sampler is named when it is not the path sampler the configs 2-5 use."""
+    return f"{METRIC_BASE}, {scene} {W}×{H}×{S}spp" + ("" if sampler == "path" else f" ({sampler} sampler)")
 
 
 def algorithmic_bytes(c: dict, shade_bytes: int, quad_scene: bool) -> int:
@@ -52,17 +58,17 @@ def shade_record_bytes(scene) -> int:
     return best
 
 
-def pmc_traffic(workload: str, kernel: str):
-    """HBM bytes per launch of `kernel` on `workload` from the committed rocprofv3 PMC summary
-    (profiles/*_traffic.json, written by scripts/pmc_traffic.py from separate --pmc passes of
-    this same bench command); None when no summary matches."""
-    for f in sorted((ROOT / "profiles").glob("*_traffic.json"), reverse=True):
+def roofline_record(workload: str, kernel: str):
+    """The committed roofline record (profiles/*_roofline/*.json, written on the GPU box by
+    scripts/roofline.py from rocprofv3 kernel-trace + PMC passes of this same bench command) for
+    this workload and kernel instance, newest round first; (None, None) when none matches."""
+    for f in sorted((ROOT / "profiles").glob("*_roofline/*.json"), reverse=True):
         try:
             d = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
-        if d.get("workload") == workload and d.get("kernel", "").replace(" ", "") == kernel:
-            return d["traffic"], f.name
+        if d.get("workload") == workload and d.get("kernel", "").replace(" ", "") == kernel.replace(" ", ""):
+            return d, str(f.relative_to(ROOT))
     return None, None
 
 
@@ -80,7 +86,8 @@ def cpu_baseline(scene_abi, params, width, height, nthreads, spp=2):
     dt = time.perf_counter() - t0
     return {"value": cnt["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": nthreads, "kind": "port",
             "sample": f"{width}x{height} x {spp} spp (samples 0..{spp - 1}) of the bench workload, "
-                      f"{cnt['rays']} rays in {dt:.2f} s"}
+                      f"{cnt['rays']} rays in {dt:.2f} s",
+            "rays": int(cnt["rays"]), "seconds": round(dt, 3)}
 
 
 def main():
@@ -121,14 +128,24 @@ def main():
     from jtrace import abi, sceneio, trace
     from jtrace.cli import Params
     lib = abi.load_library()
+    # time to first pixel, by stage (the reference's timers, src/jtrace.jl:49-65): scene load,
+    # BVH build, lights, device upload (jt_create)
+    t_0 = time.perf_counter()
     scene = sceneio.load_scene(args.scene, missing="drop")  # configs 3-5: the checkout lacks a few files
     sa = abi.SceneABI(scene)
+    t_load = time.perf_counter()
     params = Params(scene=args.scene, samples=args.spp, sampler=2 if args.sampler == "naive" else 1,
                     width=args.width, height=args.height, device=dev, batch=args.spp)
     jp = abi.make_params(params, 0)
     bvh = trace.make_scene_bvh(sa, False, lib)
+    t_bvh = time.perf_counter()
     lights = trace.make_trace_lights(sa, lib)
+    t_lights = time.perf_counter()
     state = trace.make_trace_state(sa, bvh, lights, jp, lib)
+    t_create = time.perf_counter()
+    ttfp = {"load_s": round(t_load - t_0, 3), "bvh_s": round(t_bvh - t_load, 3),
+            "lights_s": round(t_lights - t_bvh, 3), "upload_s": round(t_create - t_lights, 3),
+            "total_s": round(t_create - t_0, 3)}
     W, H, S = state.width, state.height, args.spp
     from jtrace.parallel import reduce_running_means, shard_range
     s0, s1 = shard_range(S, world, rank)
@@ -190,6 +207,22 @@ def main():
     else:
         total_rays = float(rays)
 
+    # CPU baseline leg (rank 0, N=1): the oracle on host cores over samples [0, cpu_spp) of this
+    # workload; the GPU then re-traces exactly those samples so the two ray counts — hence the
+    # two cameras and framings — are checked to agree (a libm ulp may flip a rare path: <= 0.1 %)
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(sa, jp, W, H, args.cpu_threads, args.cpu_spp)
+        state.reset()
+        state.trace_range(0, args.cpu_spp)
+        g = state.counters()
+        cpu["gpu_rays_same_samples"] = int(g["rays"])
+        cpu["rays_per_sample"] = round(cpu["rays"] / (W * H * args.cpu_spp), 6)
+        cpu["gpu_rays_per_sample"] = round(g["rays"] / (W * H * args.cpu_spp), 6)
+        if abs(g["rays"] - cpu["rays"]) > 1e-3 * cpu["rays"]:
+            raise SystemExit(f"cpu_baseline traced a different workload: {cpu['rays']} rays on the CPU vs "
+                             f"{g['rays']} on the GPU over the same samples")
+
     if rank == 0:
         name = Path(args.scene).stem
         value = total_rays / elapsed / 1e6
@@ -197,26 +230,40 @@ def main():
         launches = max(1, agg["launches"])
         avg_launch_s = kernel_ms / launches / 1e3
         per_launch = {k: v / max(1, full["launches"]) for k, v in full.items()}  # one step's launches
-        bytes_per_launch = algorithmic_bytes(per_launch, shade_record_bytes(scene),
-                                             any(len(s.quads) for s in scene.shapes))
-        achieved = bytes_per_launch / avg_launch_s / 1e9
-        workload = f"{Path(args.scene).stem} {args.sampler} {W}x{H} {s1 - s0} samples/launch"
-        traffic, traffic_src = pmc_traffic(workload, kernel)
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
+        logical = algorithmic_bytes(per_launch, shade_record_bytes(scene),
+                                    any(len(s.quads) for s in scene.shapes))
+        workload = f"{name} {args.sampler} {W}x{H} {s1 - s0} samples/launch"
+        rec, rec_src = roofline_record(workload, kernel)
+        # HBM roof with MEASURED bytes: the PMC traffic per launch of this kernel on this workload
+        # (committed record) over this run's launch time. The §8(d) algorithmic bytes are reported
+        # beside it: small scenes serve them from LDS, so they are not HBM bytes.
+        traffic = rec["derived"]["traffic_bytes"] if rec else None
+        achieved = traffic / avg_launch_s / 1e9 if traffic else None
+        binding = None
+        if rec:
+            d = rec["derived"]
+            binding = {k: d[k] for k in ("valu_issue_frac", "lane_util", "fp32_lane_frac", "td_busy_frac",
+                                         "clock_ghz") if k in d}
+            binding["resource"] = ("vector-memory return path (TD)" if d.get("td_busy_frac", 0) > d.get("valu_issue_frac", 0)
+                                   else "VALU issue of divergent waves")
+            binding["write_bytes_per_launch"] = int(d["write_bytes"])
+            binding["profiled_launch_ms"] = round(rec["duration_ns"] / 1e6, 3)
+        roof = {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": None if traffic is None else int(traffic), "source": rec_src,
                 "kernel": kernel, "launch": desc, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                "bytes_per_launch": int(bytes_per_launch),
-                "bytes_per_ray": round(bytes_per_launch / max(1.0, per_launch["rays"]), 1),
+                "binding": binding,
+                "algorithmic": {"bytes_per_launch": int(logical),
+                                "bytes_per_ray": round(logical / max(1.0, per_launch["rays"]), 1),
+                                "gbs": round(logical / avg_launch_s / 1e9, 1),
+                                "note": "SURVEY §8(d) logical bytes (node/instance/primitive/shading records); "
+                                        "served from LDS/L2, not HBM"},
                 # traversal work per closest-hit query, from the counting pass
                 "per_ray": {k: round(per_launch[k] / max(1.0, per_launch["rays"]), 3)
                             for k in ("nodes", "instances", "prims", "shades", "light_queries")}}
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(sa, jp, W, H, args.cpu_threads, args.cpu_spp)
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "metric": metric_name(name, args.sampler, W, H, S), "value": round(value, 2), "unit": "Mrays/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": f"scene: the reference's own {name} (assets/scenes/{name}), seed 0x5EED"
                     + (f"; {'; '.join(scene.notes)}" if scene.notes else ""),
@@ -226,6 +273,7 @@ def main():
             "render_s": round(ms_per_step / 1e3, 4),
             "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 2),
             "mlight_queries_per_s": round(agg["light_queries"] * world / elapsed / 1e6, 2),
+            "time_to_first_pixel_s": ttfp,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

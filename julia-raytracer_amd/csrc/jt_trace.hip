@@ -1349,6 +1349,8 @@ struct jt_ctx {
     int kmask = FT_ALL;  // feature mask of the kernel specialisation the scene runs
     int first = -1, next = 0;  // running-mean origin and next expected sample
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
+    bool failed = false;       // a launch's tile-order wait timed out: the running means are unusable
+                               // until jt_reset
     size_t lds_scene_bytes = 0;  // > 0: small-scene LDS mode
     unsigned long long launches = 0;
     double kernel_ms = 0;
@@ -2026,6 +2028,7 @@ int jt_reset(jt_ctx* c) {
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     c->first = -1;
     c->next = 0;
+    c->failed = false;
     c->launches = 0;
     c->kernel_ms = 0;
     return JT_OK;
@@ -2035,6 +2038,7 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
     if (s0 < 0 || s1 < s0) return jt::fail(JT_ERR_STATE, "invalid sample range");
     if (s0 == s1) return JT_OK;
+    if (c->failed) return jt::fail(JT_ERR_STATE, "a previous launch failed; jt_reset the context");
     if (c->first >= 0 && s0 != c->next)
         return jt::fail(JT_ERR_STATE, "samples must be accumulated in order (expected " + std::to_string(c->next) + ")");
     if (c->first < 0) c->first = s0;
@@ -2043,6 +2047,8 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     (void)hipSetDevice(c->device);
     hipError_t e = hipMemsetAsync(c->A.work, 0, (size_t)(c->tiles + NBANDS * BAND_STRIDE) * 4, c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
+    // counter [7] counts this launch's tile-order wait timeouts only
+    if ((e = hipMemsetAsync(c->A.counters + 7, 0, 8, c->stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if (c->sampler == JT_SAMPLER_NAIVE)
         e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
@@ -2060,7 +2066,10 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     c->next = s1;
     unsigned long long timeouts = 0;
     if ((e = hipMemcpy(&timeouts, c->A.counters + 7, 8, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
-    if (timeouts) return jt::fail(JT_ERR_DEVICE, "work-unit ordering wait timed out");
+    if (timeouts) {  // a wave accumulated without its predecessor chunk: the means are corrupt
+        c->failed = true;
+        return jt::fail(JT_ERR_DEVICE, "work-unit ordering wait timed out");
+    }
     return JT_OK;
 }
 
@@ -2087,6 +2096,7 @@ int jt_get_size(const jt_ctx* c, int32_t* w, int32_t* h) {
 
 int jt_get_image(jt_ctx* c, float* rgba) {
     if (!c || !rgba) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    if (c->failed) return jt::fail(JT_ERR_STATE, "the running means are corrupt (a launch failed); jt_reset the context");
     (void)hipSetDevice(c->device);
     hipError_t e = hipMemcpy(rgba, c->A.image, (size_t)c->width * c->height * 16, hipMemcpyDeviceToHost);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy image");
@@ -2094,6 +2104,7 @@ int jt_get_image(jt_ctx* c, float* rgba) {
 
 int jt_get_aovs(jt_ctx* c, float* albedo, float* normal, int64_t* hits) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    if (c->failed) return jt::fail(JT_ERR_STATE, "the running means are corrupt (a launch failed); jt_reset the context");
     (void)hipSetDevice(c->device);
     const size_t np = (size_t)c->width * c->height;
     std::vector<float4> tmp(np);

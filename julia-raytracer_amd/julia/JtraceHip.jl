@@ -95,6 +95,9 @@ check(st) = st == 0 ? nothing :
 frame12(f) = ntuple(k -> Float32(reinterpret(Float32, [f])[k]), 12)  # Frame3f = 4 x Vec3f
 f3(v) = (Float32(v[1]), Float32(v[2]), Float32(v[3]))
 ids0(v, n) = Int32[Int32(x[k] - 1) for x in v for k in 1:n]          # 1-based Int -> 0-based Int32
+# an optional id (texture, light instance/environment): 1-based, or invalid_id (-1, src/scene.jl:45)
+# for none; the C side's "none" is -1 too, so only real ids shift
+id0(x) = x == -1 ? Int32(-1) : Int32(x - 1)
 flat(v) = isempty(v) ? Float32[] : collect(reinterpret(Float32, v))
 
 # ---- packing: Julia SceneData/SceneBvh/TraceLights -> C views (arrays kept in `keep`) -----
@@ -102,10 +105,10 @@ function pack_scene(scene::SceneData, keep::Vector{Any})
     cams = [JtCamera(frame12(c.frame), c.orthographic, c.lens, c.film, c.aspect, c.focus, c.aperture)
             for c in scene.cameras]
     insts = [JtInstance(frame12(i.frame), i.shape - 1, i.material - 1) for i in scene.instances]
-    envs = [JtEnvironment(frame12(e.frame), f3(e.emission), e.emission_tex - 1) for e in scene.environments]
+    envs = [JtEnvironment(frame12(e.frame), f3(e.emission), id0(e.emission_tex)) for e in scene.environments]
     mats = [JtMaterial(Int32(Int(m.type)), f3(m.emission), f3(m.color), m.roughness, m.metallic, m.ior,
-                       f3(m.scattering), m.scanisotropy, m.trdepth, m.opacity, m.emission_tex - 1,
-                       m.color_tex - 1, m.roughness_tex - 1, m.scattering_tex - 1, m.normal_tex - 1)
+                       f3(m.scattering), m.scanisotropy, m.trdepth, m.opacity, id0(m.emission_tex),
+                       id0(m.color_tex), id0(m.roughness_tex), id0(m.scattering_tex), id0(m.normal_tex))
             for m in scene.materials]
     texs = JtTexture[]
     for t in scene.textures
@@ -152,7 +155,7 @@ function pack_lights(lights::TraceLights, keep)
     for l in lights.lights
         cdf = collect(Float32, l.elements_cdf)
         push!(keep, cdf)
-        push!(ls, JtLight(l.instance - 1, l.environment - 1, length(cdf), pointer(cdf)))
+        push!(ls, JtLight(id0(l.instance), id0(l.environment), length(cdf), pointer(cdf)))
     end
     push!(keep, ls)
     JtLights(length(ls), pointer(ls))

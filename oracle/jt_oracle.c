@@ -328,6 +328,7 @@ typedef struct {
     fr3* env_frame;
     fr3* env_inverse;  /* inverse(frame) rigid (src/scene.jl:906) */
     fr3 camera_frame;
+    float camera_aspect; /* cam.aspect, or W/H when --width/--height are given (see setup_ctx) */
     int width, height;
 } ctx_t;
 
@@ -1471,9 +1472,10 @@ static path_result trace_naive(const ctx_t* c, ray3 ray, rng_t* rng, scratch_t* 
     return res;
 }
 
-/* eval_camera (src/scene.jl:372-411) */
-static ray3 eval_camera(const jt_camera* cam, const fr3* frame, v2 image_uv, v2 lens_uv) {
-    v2 film = cam->aspect >= 1 ? V2(cam->film, cam->film / cam->aspect) : V2(cam->film * cam->aspect, cam->film);
+/* eval_camera (src/scene.jl:372-411); `aspect` is camera.aspect (:377-378), or W/H under the
+ * --width/--height extension (setup_ctx) */
+static ray3 eval_camera(const jt_camera* cam, float aspect, const fr3* frame, v2 image_uv, v2 lens_uv) {
+    v2 film = aspect >= 1 ? V2(cam->film, cam->film / aspect) : V2(cam->film * aspect, cam->film);
     if (!cam->orthographic) {
         v3 q = V3(film.x * (0.5f - image_uv.x), film.y * (image_uv.y - 0.5f), cam->lens);
         v3 dc = neg3(normalize3(q));
@@ -1494,13 +1496,13 @@ static ray3 eval_camera(const jt_camera* cam, const fr3* frame, v2 image_uv, v2 
 static ray3 sample_camera(const ctx_t* c, const jt_camera* cam, int i, int j, v2 puv, v2 luv, int tent) {
     if (!tent) {
         v2 uv = V2(((float)i + puv.x) / (float)c->width, ((float)j + puv.y) / (float)c->height);
-        return eval_camera(cam, &c->camera_frame, uv, sample_disk(luv));
+        return eval_camera(cam, c->camera_aspect, &c->camera_frame, uv, sample_disk(luv));
     }
     float width = 2.0f, offset = 0.5f;
     v2 fuv = V2(width * (puv.x < 0.5f ? sqrtf(2 * puv.x) - 1 : 1 - sqrtf(2 - 2 * puv.x)) + offset,
                 width * (puv.y < 0.5f ? sqrtf(2 * puv.y) - 1 : 1 - sqrtf(2 - 2 * puv.y)) + offset);
     v2 uv = V2(((float)i + fuv.x) / (float)c->width, ((float)j + fuv.y) / (float)c->height);
-    return eval_camera(cam, &c->camera_frame, uv, sample_disk(luv));
+    return eval_camera(cam, c->camera_aspect, &c->camera_frame, uv, sample_disk(luv));
 }
 
 typedef struct {
@@ -1588,6 +1590,12 @@ static int setup_ctx(ctx_t* c, const jt_scene* scene, const jt_scene_bvh* bvh, c
     c->height = height;
     if (params->camera < 0 || params->camera >= scene->ncameras) return JT_ERR_INVALID;
     c->camera_frame = frame_from(scene->cameras[params->camera].frame);
+    /* The reference sizes the film from camera.aspect only (src/scene.jl:377-378, src/trace.jl:189-197
+     * derives W,H from it). The build's --width/--height extension renders an explicit W x H frame
+     * (the 1280x720 headline config of a 1:1 cornellbox camera) and fits the film to it:
+     * aspect := W/H (float division), as jt_create does (jt_trace.hip, DParams.cam.aspect). */
+    c->camera_aspect = (params->width > 0 && params->height > 0) ? (float)width / (float)height
+                                                                 : scene->cameras[params->camera].aspect;
     c->inst_frame = (fr3*)malloc(sizeof(fr3) * (size_t)(scene->ninstances + 1));
     c->inst_inverse = (fr3*)malloc(sizeof(fr3) * (size_t)(scene->ninstances + 1));
     c->env_frame = (fr3*)malloc(sizeof(fr3) * (size_t)(scene->nenvironments + 1));

@@ -1,0 +1,140 @@
+"""Roofline record of the timed trace kernel from rocprofv3 runs of one bench command, and its
+re-check from the committed record alone.
+
+The trace kernel is a divergent, pointer-chasing path (no MFMA). Its roof is
+stated against HBM as the contract asks (`bound: "hbm"`), with the MEASURED HBM bytes — not the
+algorithmic §8(d) bytes, which small scenes serve from LDS — and beside it the resource that
+actually binds, computed from PMC counters the same way for every workload:
+
+  clock_hz        = GRBM_GUI_ACTIVE / 8 XCDs / duration      (GRBM_GUI_ACTIVE sums the XCDs)
+  valu_issue_frac = SQ_INSTS_VALU / (CUs * 4 SIMDs * 0.5 wave-instr/clk * clock_hz * duration)
+  lane_util       = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)
+  fp32_lane_frac  = valu_issue_frac * lane_util               (fraction of the FP32 lane throughput)
+  td_busy_frac    = TD_TD_BUSY_sum / CUs / (GRBM_GUI_ACTIVE / 8)   (mean busy fraction of a CU's TD)
+  hbm_frac        = (2 * FETCH_SIZE + WRITE_SIZE) KiB * 1024 / duration / 8e12   (MI355X_MICROARCH.md)
+
+usage:
+  python scripts/roofline.py make --stats KT.csv --fetch DIR --write DIR [--pmc DIR] --workload W --out OUT.json
+  python scripts/roofline.py check OUT.json [...]      # recompute every derived field, exit 1 on mismatch
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import re
+import sys
+
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
+CUS = 256
+XCDS = 8
+KERNEL_RE = re.compile(r"(trace_kernel\w*<\d+, \d+, (?:true|false), 0, \d+>)")
+
+
+def timed_kernel(stats_csv):
+    best = None
+    for r in csv.DictReader(open(stats_csv)):
+        m = KERNEL_RE.search(r["Name"])
+        if m and (best is None or float(r["TotalDurationNs"]) > best[0]):
+            best = (float(r["TotalDurationNs"]), m.group(1), float(r["AverageNs"]), int(r["Calls"]))
+    if best is None:
+        raise SystemExit(f"no COUNT=0 trace kernel in {stats_csv}")
+    return best[1], best[2], best[3]
+
+
+def counter_means(d, kernel):
+    """Per-dispatch sums of every counter of `kernel` (summed over the counter's dimensions),
+    averaged over dispatches; plus the mean dispatch duration of those runs."""
+    per = {}
+    durs = {}
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel not in r["Kernel_Name"].replace("(anonymous namespace)::", ""):
+                continue
+            key = (f, r["Dispatch_Id"])
+            per.setdefault(r["Counter_Name"], {}).setdefault(key, 0.0)
+            per[r["Counter_Name"]][key] += float(r["Counter_Value"])
+            durs[key] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    means = {c: sum(v.values()) / len(v) for c, v in per.items()}
+    return means, (sum(durs.values()) / len(durs) if durs else None)
+
+
+def derive(rec):
+    """Every derived field from the raw ones (used by make and by check)."""
+    raw, out = rec["raw"], {}
+    dur = rec["duration_ns"] * 1e-9
+    traffic = 2.0 * raw["FETCH_SIZE"] * 1024.0 + raw["WRITE_SIZE"] * 1024.0
+    out["traffic_bytes"] = traffic
+    out["write_bytes"] = raw["WRITE_SIZE"] * 1024.0
+    out["hbm_gbs"] = traffic / dur / 1e9
+    out["hbm_frac"] = traffic / dur / HBM_PEAK
+    pmc = rec.get("pmc") or {}
+    if pmc.get("GRBM_GUI_ACTIVE") and pmc.get("pmc_duration_ns"):
+        pd = pmc["pmc_duration_ns"] * 1e-9
+        clk = pmc["GRBM_GUI_ACTIVE"] / XCDS / pd
+        out["clock_ghz"] = clk / 1e9
+        if pmc.get("SQ_INSTS_VALU"):
+            out["valu_issue_frac"] = pmc["SQ_INSTS_VALU"] / (CUS * 4 * 0.5 * clk * pd)
+        if pmc.get("SQ_THREAD_CYCLES_VALU") and pmc.get("SQ_ACTIVE_INST_VALU"):
+            out["lane_util"] = pmc["SQ_THREAD_CYCLES_VALU"] / (64.0 * pmc["SQ_ACTIVE_INST_VALU"])
+        if "valu_issue_frac" in out and "lane_util" in out:
+            out["fp32_lane_frac"] = out["valu_issue_frac"] * out["lane_util"]
+        if pmc.get("TD_TD_BUSY_sum"):  # summed over the 256 CUs' TD units
+            out["td_busy_frac"] = pmc["TD_TD_BUSY_sum"] / CUS / (pmc["GRBM_GUI_ACTIVE"] / XCDS)
+    return {k: round(v, 6) for k, v in out.items()}
+
+
+def make(a):
+    kernel, avg_ns, calls = timed_kernel(a.stats)
+    f, _ = counter_means(a.fetch, kernel)
+    w, _ = counter_means(a.write, kernel)
+    if "FETCH_SIZE" not in f or "WRITE_SIZE" not in w:
+        raise SystemExit("FETCH_SIZE / WRITE_SIZE of the timed kernel not found")
+    rec = {"workload": a.workload, "kernel": kernel, "duration_ns": avg_ns, "calls": calls,
+           "raw": {"FETCH_SIZE": f["FETCH_SIZE"], "WRITE_SIZE": w["WRITE_SIZE"]}}
+    if a.pmc:
+        pmc, pdur = {}, []
+        for d in sorted(glob.glob(f"{a.pmc}/p*/")):
+            m, dd = counter_means(d, kernel)
+            pmc.update(m)
+            if dd:
+                pdur.append(dd)
+        if pdur:
+            pmc["pmc_duration_ns"] = sum(pdur) / len(pdur)
+        rec["pmc"] = pmc
+    rec["derived"] = derive(rec)
+    json.dump(rec, open(a.out, "w"), indent=1)
+    print(json.dumps(rec["derived"]))
+
+
+def check(paths):
+    bad = 0
+    for p in paths:
+        rec = json.load(open(p))
+        again = derive(rec)
+        for k, v in again.items():
+            if abs(rec["derived"].get(k, float("nan")) - v) > 1e-6 * max(1.0, abs(v)):
+                print(f"{p}: {k} recorded {rec['derived'].get(k)} recomputed {v}")
+                bad += 1
+        if again["hbm_frac"] > 1.0:
+            print(f"{p}: hbm_frac {again['hbm_frac']} > 1")
+            bad += 1
+        print(p, json.dumps(again))
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    m = sub.add_parser("make")
+    m.add_argument("--stats", required=True)
+    m.add_argument("--fetch", required=True)
+    m.add_argument("--write", required=True)
+    m.add_argument("--pmc")
+    m.add_argument("--workload", required=True)
+    m.add_argument("--out", required=True)
+    c = sub.add_parser("check")
+    c.add_argument("paths", nargs="+")
+    a = ap.parse_args()
+    make(a) if a.cmd == "make" else check(a.paths)

@@ -277,3 +277,32 @@ def test_device_buffer_view_is_the_running_mean(gpu, abi, lib, cornell_abi):
     out = reduce_running_means(dev, 3, 3, _OneRank, dst=0)
     np.testing.assert_allclose(out.cpu().numpy(), host, rtol=1e-6, atol=0)
     st.close()
+
+
+def _full_parity(abi, lib, oracle, scene_abi, params, spp, label):
+    g, o = _render_both(abi, lib, oracle, scene_abi, params, 0, spp)
+    stats = compare_images(g[0], o[0])
+    print(label, g[0].shape, stats, "gpu", g[4], "oracle", o[4])
+    assert stats["frac_pix_rel_le_1e-3"] >= 0.999, stats
+    assert stats["image_mean_rel"] <= 1e-4, stats
+    assert np.array_equal(g[3], o[3])
+    H, W = g[0].shape[:2]
+    assert g[4]["paths"] == o[4]["paths"] == W * H * spp
+    for k in ("rays", "light_queries", "nodes", "instances", "prims", "shades"):
+        assert abs(g[4][k] - o[4][k]) <= 1e-3 * o[4][k] + 8, (k, g[4][k], o[4][k])
+    for a, b in zip(g[1:3], o[1:3]):
+        assert compare_images(a, b)["frac_pix_rel_le_1e-3"] >= 0.999
+
+
+def test_headline_frame_parity(gpu, abi, lib, oracle, cornell_abi):
+    """The bench's exact framing — cornellbox path at 1280x720 through --width/--height, whose
+    film is fitted to W/H (the oracle restates that override) — against the oracle, full frame,
+    8 spp (the headline workload's first 8 samples of every pixel)."""
+    params = make_params(abi, width=1280, height=720, samples=8, sampler=1)
+    _full_parity(abi, lib, oracle, cornell_abi, params, 8, "cornellbox path 1280x720x8")
+
+
+def test_config1_full_size_parity(gpu, abi, lib, oracle, cornell_abi):
+    """BASELINE config 1 at its own size: cornellbox naive 256x256 x 16 spp (1,048,576 paths)."""
+    params = make_params(abi, resolution=256, samples=16, sampler=2)
+    _full_parity(abi, lib, oracle, cornell_abi, params, 16, "config1 cornellbox naive 256x256x16")
