@@ -244,7 +244,9 @@ def main():
             d = rec["derived"]
             binding = {k: d[k] for k in ("valu_issue_frac", "lane_util", "fp32_lane_frac", "td_busy_frac",
                                          "clock_ghz") if k in d}
-            binding["resource"] = ("vector-memory return path (TD)" if d.get("td_busy_frac", 0) > d.get("valu_issue_frac", 0)
+            # LDS mode (small scenes): the scene is in LDS, VALU issue of partly idle waves binds;
+            # HBM mode: node/primitive loads through the vector-memory return path (TD) bind
+            binding["resource"] = ("vector-memory return path (TD)" if "mode=hbm" in desc
                                    else "VALU issue of divergent waves")
             binding["write_bytes_per_launch"] = int(d["write_bytes"])
             binding["profiled_launch_ms"] = round(rec["duration_ns"] / 1e6, 3)
