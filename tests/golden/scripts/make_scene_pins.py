@@ -1,9 +1,10 @@
 """Generates tests/golden/scene_pins.npz from the reference's own renders
 /root/reference/images/<scene>_<sampler>.png (RGBA8 sRGB, spp unrecorded) for the scenes
 shipped under assets/scenes (features1, features2, materials1, materials2, materials4, shapes1
-at 1280x533, bathroom1 at 1280x720, ecosys at 1280x640; both samplers).
+at 1280x533, bathroom1 at 1280x720, ecosys at 1280x640, coffee at 1024x1280, staircase2 at
+1280x1280; both samplers).
 
-The fixture is data only: per block (41 or 40 rows x 40 columns) the mean of the
+The fixture is data only: per block (41 or 40 rows x 40 or 32 columns) the mean of the
 sRGB-decoded linear values per channel, the block alpha mean and the whole-image channel mean.
 It is the statistical pin of the HIP path on these scenes (tests/test_gpu_scenes.py).
 Run in the build container (the reference is not on the GPU box):
@@ -14,9 +15,9 @@ import os
 import numpy as np
 from PIL import Image
 
-SCENES = ("features1", "features2", "materials1", "materials2", "materials4", "shapes1", "bathroom1", "ecosys")
+SCENES = ("features1", "features2", "materials1", "materials2", "materials4", "shapes1", "bathroom1", "ecosys",
+          "coffee", "staircase2")
 OUT = os.path.join(os.path.dirname(__file__), "..", "scene_pins.npz")
-BW = 40
 
 out = {}
 for scene in SCENES:
@@ -25,6 +26,7 @@ for scene in SCENES:
                          dtype=np.uint8)
         h, w = img.shape[:2]
         BH = 41 if h % 41 == 0 else 40
+        BW = 40 if w % 40 == 0 else 32  # coffee is 1024 wide
         assert h % BH == 0 and w % BW == 0, (scene, h, w)
         c = img[..., :3].astype(np.float64) / 255.0
         lin = np.where(c <= 0.04045, c / 12.92, ((c + 0.055) / 1.055) ** 2.4)

@@ -12,6 +12,8 @@ Scene coverage of SURVEY.md §8(a):
   bathroom1  config 4 (855 instances, 572 K triangles; 3 textures missing in the checkout:
              invalid_id, i.e. constant (1,1,1,1))
   ecosys     config 5 (12.7 K instances of 139 shapes; shape002/003 missing: dropped)
+  coffee     complete scene: glossy, refractive glass, reflective metal (235 K triangles)
+  staircase2 complete scene: glossy/reflective/refractive, textured (31 K triangles)
 Tolerance as tests/test_gpu_parity.py (>= 99.9 % of pixels within 1e-3 relative; image mean
 within 1e-4 relative).
 """
@@ -24,7 +26,8 @@ from conftest import CORNELL, ROOT, compare_images, make_params
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ("features1", "features2", "materials1", "materials2", "materials4", "shapes1", "bathroom1", "ecosys")
+SCENES = ("features1", "features2", "materials1", "materials2", "materials4", "shapes1", "bathroom1", "ecosys",
+          "coffee", "staircase2")
 # The reference renders of these scenes hold data the checkout lacks, so the pin is loose:
 # (channel-mean rtol, block-median bound). features2: two dropped shapes; bathroom1: three
 # missing textures rendered as constant (1,1,1,1) (the renders are ~6 % brighter); ecosys:

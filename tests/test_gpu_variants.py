@@ -1,0 +1,80 @@
+"""HIP path vs the oracle on synthetic variants of cornellbox that reach branches no shipped
+config scene takes (VERDICT r01 "What's missing" 4):
+  - thin lens, aperture > 0: eval_camera's lens sample through sample_disk
+    (src/scene.jl:372-411, src/sampling.jl:12-16) instead of the pinhole sign shortcut;
+  - the orthographic camera branch of eval_camera;
+  - vertex colours: eval_color's barycentric interpolation (src/scene.jl:690-720), multiplying
+    the material colour, and its alpha entering the opacity (src/scene.jl:649) — with alphas
+    below 1 the opacity draw and the opacity retry (src/trace.jl:336-345) run too.
+Same bar as tests/test_gpu_parity.py.
+"""
+import copy
+
+import numpy as np
+import pytest
+
+from conftest import compare_images, make_params
+
+pytestmark = pytest.mark.gpu
+
+
+def _parity(abi, lib, oracle, scene, label, sampler=1, spp=6, res=96):
+    from jtrace import trace
+    sa = abi.SceneABI(scene)
+    p = make_params(abi, resolution=res, samples=spp, sampler=sampler)
+    bvh = trace.make_scene_bvh(sa, False, lib)
+    lights = trace.make_trace_lights(sa, lib)
+    st = trace.make_trace_state(sa, bvh, lights, p, lib)
+    st.set_counters(1)
+    st.trace_range(0, spp)
+    g = (st.get_image(), *st.get_aovs(), st.counters(), st.describe())
+    st.close()
+    o = oracle.trace(sa, oracle.build_bvh(sa), oracle.make_lights(sa), p, g[0].shape[1], g[0].shape[0], 0, spp)
+    stats = compare_images(g[0], o[0])
+    print(label, g[5], stats, "gpu", g[4], "oracle", o[4])
+    assert stats["frac_pix_rel_le_1e-3"] >= 0.999, (label, stats)
+    assert stats["image_mean_rel"] <= 1e-4, (label, stats)
+    assert np.array_equal(g[3], o[3]), label
+    for k in ("rays", "light_queries", "nodes", "instances", "prims", "shades"):
+        assert abs(g[4][k] - o[4][k]) <= 1e-3 * o[4][k] + 8, (label, k, g[4][k], o[4][k])
+    for a, b in ((g[1], o[1]), (g[2], o[2])):
+        assert compare_images(a, b)["frac_pix_rel_le_1e-3"] >= 0.999, label
+    return g, o
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
+def test_thin_lens_camera_parity(gpu, abi, lib, oracle, cornell, sampler):
+    sc = copy.deepcopy(cornell)
+    sc.cameras[0].aperture = np.float32(0.25)  # strong defocus: focus 3.9 on the back wall
+    g, o = _parity(abi, lib, oracle, sc, f"aperture/{sampler}", sampler=sampler)
+    # the lens really is sampled: the defocused render differs from the pinhole one
+    p0 = copy.deepcopy(cornell)
+    from jtrace import trace
+    sa = abi.SceneABI(p0)
+    p = make_params(abi, resolution=96, samples=6, sampler=sampler)
+    st = trace.make_trace_state(sa, trace.make_scene_bvh(sa, False, lib), trace.make_trace_lights(sa, lib), p, lib)
+    st.trace_range(0, 6)
+    assert not np.array_equal(st.get_image(), g[0])
+    st.close()
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
+def test_orthographic_camera_parity(gpu, abi, lib, oracle, cornell, sampler):
+    sc = copy.deepcopy(cornell)
+    sc.cameras[0].orthographic = True
+    sc.cameras[0].lens = np.float32(0.02)  # film/lens scale: a ~1.2-unit wide view of the box
+    g, o = _parity(abi, lib, oracle, sc, f"ortho/{sampler}", sampler=sampler)
+    assert g[3].sum() > 0  # it sees the scene
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
+def test_vertex_colors_parity(gpu, abi, lib, oracle, cornell, sampler):
+    sc = copy.deepcopy(cornell)
+    rng = np.random.default_rng(7)
+    for k, s in enumerate(sc.shapes):
+        n = len(s.positions)
+        col = rng.uniform(0.2, 1.0, size=(n, 4)).astype(np.float32)
+        col[:, 3] = 1.0 if k % 2 else rng.uniform(0.6, 1.0, size=n).astype(np.float32)
+        s.colors = col
+    g, o = _parity(abi, lib, oracle, sc, f"vcolor/{sampler}", sampler=sampler)
+    assert ",255> " in g[5]  # FT_ATTR | FT_OPAC: the general kernel
