@@ -155,6 +155,7 @@ struct DParams {
     int light_lanes;  // path sampler: run a light-hit step inside the traversal phase once this
                       // many lanes wait on a sample_lights_pdf query result (65: never)
     int chunk;  // samples per work unit (a tile's chunks run in order)
+    int wf_groups;  // WF body: 64-slot path groups per workgroup
     unsigned long long seed;
 };
 

@@ -671,8 +671,34 @@ __device__ __forceinline__ void aov_update(const Aov& a, v3 ta, v3 tn) {
     p[9 * BLOCK] = p[9 * BLOCK] * omw + tn.z * aw;
 }
 
+// The WF body's accessor (trace_body_wf): the pixel's albedo / normal running means are read-
+// modified-written in HBM (each pixel has one owning path slot, whose samples run in order),
+// with the same float operations as aov_update's LDS form.
+struct WfAov {
+    float4* albedo;
+    float4* normal;
+    int pixel;
+    float w_;
+    template <int F>
+    __device__ __forceinline__ float w() const { return w_; }
+};
 template <int F>
-__device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const Aov& aov,
+__device__ __forceinline__ void aov_update(const WfAov& a, v3 ta, v3 tn) {
+    const float aw = a.w_;
+    const float omw = 1 - aw;
+    float4 al = a.albedo[a.pixel], nr = a.normal[a.pixel];
+    al.x = al.x * omw + ta.x * aw;
+    al.y = al.y * omw + ta.y * aw;
+    al.z = al.z * omw + ta.z * aw;
+    nr.x = nr.x * omw + tn.x * aw;
+    nr.y = nr.y * omw + tn.y * aw;
+    nr.z = nr.z * omw + tn.z * aw;
+    a.albedo[a.pixel] = al;
+    a.normal[a.pixel] = nr;
+}
+
+template <int F, class AovT>
+__device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const AovT& aov,
                                          unsigned& shades) {
     if (!isec.hit) {
         if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
@@ -770,8 +796,8 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
 }
 
 // trace_naive's bounce body after the closest-hit query (src/trace.jl:490-569)
-template <int F>
-__device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const Aov& aov,
+template <int F, class AovT>
+__device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const AovT& aov,
                                           unsigned& shades) {
     if (!isec.hit) {
         if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
@@ -882,6 +908,8 @@ struct DAccum {
     unsigned* work;                // unit counters of the launch, one per XCD band at work[16 b]
                                    // (zeroed before each launch)
     int* tile_done;                // per 8x8 tile: sample chunks accumulated in this launch
+    float4* pool;                  // WF body: path-slot records (HBM), pool_bytes long
+    size_t pool_bytes;
 };
 
 // Work units: (sample chunk c, 8x8 pixel tile t), fetched by whole waves from atomic counters,
@@ -1189,6 +1217,439 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     }
 }
 
+// ============================================================================ WF body
+// trace_samples with the queries decoupled from the paths (DESIGN.md §2 "WF scheduling"). A
+// workgroup owns P = 64 * G path slots, G slot groups of one 8x8 tile x sample chunk each (more
+// paths than its 256 lanes). A slot's path state lives in a 128/160-B record in HBM (L2) between
+// shading steps; its pending BVH query (origin, direction, root) in LDS. Three LDS rings hold
+// slot ids: queries waiting for a lane, scene results and light results waiting for shading.
+// Every iteration each wave picks one wave-uniform job:
+//   - start an idle group on a new work unit (64 new paths, one per lane);
+//   - shade a batch of up to 64 waiting results (scene or light ring): load the slot's path,
+//     path_hit / naive_hit / light_hit, issue its next query or finish its sample;
+//   - traverse: lanes without a query take one from the ring, then one node/primitive step kind.
+// A lane's query runs on that lane to completion (its stack is the lane's LDS stack), but any
+// lane may run any slot's query, and any wave may shade any slot: traversal steps run on nearly
+// full waves and shading steps on full batches, instead of the idle lanes a per-lane path
+// leaves while it waits. Each path's float operations and RNG draws are the reference's, in its
+// order, and a pixel's samples are accumulated in order (one slot per pixel and chunk; chunks of
+// a tile in order, as trace_body): results are bit-identical to trace_body.
+constexpr int WF_GMAX = 8;
+constexpr int WF_TRAV = 0, WF_SCENE = 1, WF_LIGHT = 2;
+struct WfCtl {
+    unsigned head[3], tail[3];
+    int g_tile[WF_GMAX], g_uc[WF_GMAX], g_cs1[WF_GMAX];
+    int g_left[WF_GMAX];  // -1 idle, -2 unit assigned and waiting for its tile's previous chunk, >= 0 slots running
+    int band_k;
+    int exhausted;        // every band's units handed out
+};
+__host__ __device__ constexpr int wf_rec_q(int F) { return (F & FT_VOL) ? 10 : 8; }  // float4s per slot record
+
+template <int F>
+__device__ __forceinline__ void wf_store(float4* r, const Path& st, int pixel, int sample) {
+    const unsigned long long s = st.rng.state, c = st.rng.inc;
+    r[0] = make_float4(st.o.x, st.o.y, st.o.z, st.d.x);
+    r[1] = make_float4(st.d.y, st.d.z, st.radiance.x, st.radiance.y);
+    r[2] = make_float4(st.radiance.z, st.weight.x, st.weight.y, st.weight.z);
+    r[3] = make_float4(__uint_as_float((unsigned)s), __uint_as_float((unsigned)(s >> 32)), __uint_as_float((unsigned)c),
+                       __uint_as_float((unsigned)(c >> 32)));
+    r[4] = make_float4(__int_as_float(st.bounce), __int_as_float(st.opbounce), __int_as_float(st.flags | st.phase << 8),
+                       st.max_roughness);
+    r[5] = make_float4(__int_as_float(st.li), __int_as_float(st.lcount), st.pb, st.pdf);
+    r[6] = make_float4(st.lpdf, st.lq.x, st.lq.y, st.lq.z);
+    r[7] = make_float4(__int_as_float(pixel), __int_as_float(sample), 0.0f, 0.0f);
+    if (F & FT_VOL) {
+        r[8] = make_float4(st.vol.density.x, st.vol.density.y, st.vol.density.z, st.vol.scattering.x);
+        r[9] = make_float4(st.vol.scattering.y, st.vol.scattering.z, st.vol.scanisotropy, 0.0f);
+    }
+}
+template <int F>
+__device__ __forceinline__ void wf_load(const float4* r, Path& st, int& pixel, int& sample) {
+    const float4 a = r[0], b = r[1], c = r[2], d = r[3], e = r[4], f = r[5], g = r[6], h = r[7];
+    st.o = V3(a.x, a.y, a.z);
+    st.d = V3(a.w, b.x, b.y);
+    st.radiance = V3(b.z, b.w, c.x);
+    st.weight = V3(c.y, c.z, c.w);
+    st.rng.state = (unsigned long long)__float_as_uint(d.x) | (unsigned long long)__float_as_uint(d.y) << 32;
+    st.rng.inc = (unsigned long long)__float_as_uint(d.z) | (unsigned long long)__float_as_uint(d.w) << 32;
+    st.bounce = __float_as_int(e.x);
+    st.opbounce = __float_as_int(e.y);
+    st.flags = __float_as_int(e.z) & 0xff;
+    st.phase = __float_as_int(e.z) >> 8;
+    st.max_roughness = e.w;
+    st.li = __float_as_int(f.x);
+    st.lcount = __float_as_int(f.y);
+    st.pb = f.z;
+    st.pdf = f.w;
+    st.lpdf = g.x;
+    st.lq = V3(g.y, g.z, g.w);
+    pixel = __float_as_int(h.x);
+    sample = __float_as_int(h.y);
+    if (F & FT_VOL) {
+        const float4 v0 = r[8], v1 = r[9];
+        st.vol.density = V3(v0.x, v0.y, v0.z);
+        st.vol.scattering = V3(v0.w, v1.x, v1.y);
+        st.vol.scanisotropy = v1.z;
+    }
+}
+
+__device__ __forceinline__ int lane_rank(unsigned long long m) {  // active lanes of m below this lane
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+// claim up to `want` entries of ring q (wave-uniform result); the entries are then read with wf_take
+__device__ __forceinline__ int wf_claim(WfCtl& C, int q, int want, unsigned& base) {
+    unsigned h = 0;
+    int n = 0;
+    if ((threadIdx.x & 63) == 0) {
+        for (;;) {
+            h = __hip_atomic_load(&C.head[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const unsigned t = __hip_atomic_load(&C.tail[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            n = (int)(t - h) < want ? (int)(t - h) : want;
+            if (n <= 0) {
+                n = 0;
+                break;
+            }
+            unsigned expect = h;
+            if (__hip_atomic_compare_exchange_strong(&C.head[q], &expect, h + (unsigned)n, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                break;
+        }
+    }
+    base = __builtin_amdgcn_readfirstlane(h);
+    return __builtin_amdgcn_readfirstlane(n);
+}
+// entry `idx` of a ring: its producer reserved it before writing it, so wait for the write
+__device__ __forceinline__ int wf_take(int* ring, unsigned idx) {
+    int s;
+    while ((s = __hip_atomic_load(ring + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) __builtin_amdgcn_s_sleep(1);
+    __hip_atomic_store(ring + idx, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return s;
+}
+// push this lane's slot onto ring q when `pred`; everything the consumer reads (LDS query / result,
+// the HBM record) was written before: workgroup-scope release first
+__device__ __forceinline__ void wf_push(WfCtl& C, int* ring, int P, int q, bool pred, int slot) {
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(pred);
+    if (!m) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    unsigned base = 0;
+    if ((threadIdx.x & 63) == 0) base = __hip_atomic_fetch_add(&C.tail[q], (unsigned)lane_count(m), __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (pred) __hip_atomic_store(ring + (base + (unsigned)lane_rank(m)) % (unsigned)P, slot, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int SAMPLER, int COUNT, int F, bool NCACHE>
+__device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A, int* stack,
+                              int* lds_wf, float4* pool) {
+    constexpr int RQ = wf_rec_q(F);
+    const int lane = threadIdx.x & 63;
+    const int G = P.wf_groups, NP = 64 * G;
+    __shared__ WfCtl C;
+    int* const ring[3] = {lds_wf, lds_wf + NP, lds_wf + 2 * NP};
+    float4* const q_o = reinterpret_cast<float4*>(lds_wf + 3 * NP);  // o.xyz, root bits
+    float4* const q_d = q_o + NP;                                       // d.xyz
+    float4* const r_h = q_d + NP;                                       // inst, elem, u, v
+    float* const r_t = reinterpret_cast<float*>(r_h + NP);              // t
+    float4* const recs = pool + (size_t)blockIdx.x * NP * RQ;
+    if (threadIdx.x < 3) {
+        C.head[threadIdx.x] = 0;
+        C.tail[threadIdx.x] = 0;
+    }
+    if (threadIdx.x < WF_GMAX) C.g_left[threadIdx.x] = -1;
+    if (threadIdx.x == 0) {
+        C.band_k = 0;
+        C.exhausted = 0;
+    }
+    for (int k = threadIdx.x; k < 3 * NP; k += BLOCK) lds_wf[k] = -1;
+    __syncthreads();
+
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    const int tiles_x = (P.width + 7) / 8, tiles = tiles_x * ((P.height + 7) / 8);
+    const int nchunks = (s_end - s_begin + P.chunk - 1) / P.chunk;
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    Trav T;
+    T.sp = 0;
+    T.nprim = 0;
+    int qslot = -1;  // the slot whose query this lane runs (-1: none); bit 16: a light query
+    unsigned idle_iters = 0;
+
+    // a slot's pending query: written to LDS, then its id pushed onto the traversal ring
+    auto issue = [&](int s, const Path& st) {
+        const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
+        const v3 o = light ? st.lq : st.o;
+        const unsigned root = light ? (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance
+                                    : (T_TLAS << 30) | SNAP_NONE;
+        q_o[s] = make_float4(o.x, o.y, o.z, __uint_as_float(root));
+        q_d[s] = make_float4(st.d.x, st.d.y, st.d.z, 0.0f);
+        if (light) cnt.light_queries++;
+        else cnt.rays++;
+    };
+    // trace_sample's epilogue (src/trace.jl:625-648) for the slot's pixel: HBM read-modify-write
+    auto finish = [&](Path& st, int pixel, int sample, const WfAov& aov) {
+        cnt.paths++;
+        v3 radiance = st.radiance;
+        if (!all_finite(radiance)) radiance = V3(0, 0, 0);
+        const float mr = max3(radiance);
+        if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
+        const float w = aov.w_;
+        const float omw = 1 - w;
+        const bool hit = st.flags & F_HIT;
+        const bool env = !hit && !P.envhidden && S.nenvs != 0;
+        const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
+        if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
+        float4 im = A.image[pixel];
+        im.x = im.x * omw + target.x * w;
+        im.y = im.y * omw + target.y * w;
+        im.z = im.z * omw + target.z * w;
+        im.w = im.w * omw + target.w * w;
+        A.image[pixel] = im;
+        if (hit || env) A.hits[pixel] += 1;
+        (void)sample;
+    };
+
+    for (;;) {
+        // ---------------------------------------------------------------- pick the wave's job
+        int job = 0;        // 0 traverse, 1 start group, 2 shade scene ring, 3 shade light ring, 4 exit, 5 idle
+        int gsel = -1;
+        unsigned tl = 0, sl = 0, ll = 0;
+        const unsigned long long busy_m = __builtin_amdgcn_ballot_w64(qslot >= 0);
+        const int busy = lane_count(busy_m);
+        auto ld = [](unsigned* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+        const bool exhausted = __hip_atomic_load(&C.exhausted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+        if (lane == 0) {
+            tl = ld(&C.tail[0]) - ld(&C.head[0]);
+            sl = ld(&C.tail[1]) - ld(&C.head[1]);
+            ll = ld(&C.tail[2]) - ld(&C.head[2]);
+            // a group waiting for its tile's previous chunk, or an idle group while units remain
+            for (int g = 0; g < G && gsel < 0; g++) {
+                const int gl = __hip_atomic_load(&C.g_left[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (gl == -2) {
+                    if (__hip_atomic_load(A.tile_done + C.g_tile[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= C.g_uc[g]) {
+                        int expect = -2;
+                        if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
+                            gsel = g;
+                    }
+                } else if (gl == -1 && !exhausted) {
+                    int expect = -1;
+                    if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -4, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP))
+                        gsel = g;
+                }
+            }
+        }
+        gsel = __builtin_amdgcn_readfirstlane(gsel);
+        tl = __builtin_amdgcn_readfirstlane(tl);
+        sl = __builtin_amdgcn_readfirstlane(sl);
+        ll = __builtin_amdgcn_readfirstlane(ll);
+        const unsigned qmax = sl > ll ? sl : ll;
+        if (gsel >= 0) job = 1;
+        else if (qmax >= (unsigned)P.wait_lanes || (qmax > 0 && tl == 0 && (unsigned)busy < qmax)) job = sl >= ll ? 2 : 3;
+        else if (busy > 0 || tl > 0) job = 0;
+        else if (qmax > 0) job = sl >= ll ? 2 : 3;
+        else {
+            bool done = false;
+            if (lane == 0) {
+                done = exhausted;
+                for (int g = 0; g < G; g++)
+                    done = done && __hip_atomic_load(&C.g_left[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == -1;
+            }
+            job = __builtin_amdgcn_readfirstlane((int)done) ? 4 : 5;
+        }
+        if (job == 4) break;
+        if (job == 5) {  // other waves hold this workgroup's last queries / a tile wait: bounded wait
+            __builtin_amdgcn_s_sleep(4);
+            if (++idle_iters > (1u << 26)) {
+                if (lane == 0) atomicAdd(A.counters + 7, 1ull);
+                break;
+            }
+            continue;
+        }
+        idle_iters = 0;
+
+        if (job == 1) {
+            // ------------------------------------------------------------ start a slot group
+            int g = gsel;
+            int claimed_left = 0;
+            if (lane == 0) claimed_left = C.g_left[g];
+            claimed_left = __builtin_amdgcn_readfirstlane(claimed_left);
+            if (claimed_left == -4) {  // idle group: fetch a unit (XCD band first, then the others)
+                int unit_uc = -1, unit_t = 0;
+                if (lane == 0) {
+                    for (;;) {
+                        const int bk = __hip_atomic_load(&C.band_k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (bk >= NBANDS) break;
+                        const int band = (int)((xcc + (unsigned)bk) & (NBANDS - 1));
+                        const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
+                        const unsigned unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
+                        if (unit < (unsigned)bn * (unsigned)nchunks) {
+                            unit_uc = (int)(unit / (unsigned)bn);
+                            unit_t = bt0 + (int)(unit % (unsigned)bn);
+                            break;
+                        }
+                        int expect = bk;
+                        __hip_atomic_compare_exchange_strong(&C.band_k, &expect, bk + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    if (unit_uc < 0) {
+                        __hip_atomic_store(&C.exhausted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        C.g_tile[g] = unit_t;
+                        C.g_uc[g] = unit_uc;
+                        const int cs0 = s_begin + unit_uc * P.chunk;
+                        C.g_cs1[g] = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
+                        if (unit_uc > 0 && __hip_atomic_load(A.tile_done + unit_t, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT) < unit_uc) {
+                            __hip_atomic_store(&C.g_left[g], -2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            unit_uc = -2;  // started later, when the previous chunk is published
+                        }
+                    }
+                }
+                unit_uc = __builtin_amdgcn_readfirstlane(unit_uc);
+                if (unit_uc < 0) continue;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const int ut = C.g_tile[g], uc = C.g_uc[g];
+            if (uc > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's running means
+            const int i = (ut % tiles_x) * 8 + (lane & 7), j = (ut / tiles_x) * 8 + (lane >> 3);
+            const bool in_image = i < P.width && j < P.height;
+            const int s = g * 64 + lane;
+            const int cs0 = s_begin + uc * P.chunk;
+            const int pixel = j * P.width + i;
+            if (in_image) {
+                Path st;
+                start_path(P, i, j, pixel, cs0, st);
+                wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0);
+                issue(s, st);
+            }
+            if (lane == 0)
+                __hip_atomic_store(&C.g_left[g], lane_count(__builtin_amdgcn_ballot_w64(in_image)), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            wf_push(C, ring[WF_TRAV], NP, WF_TRAV, in_image, s);
+            continue;
+        }
+
+        if (job >= 2) {
+            // ------------------------------------------------------------ shade a batch
+            const int q = job == 2 ? WF_SCENE : WF_LIGHT;
+            unsigned base;
+            const int n = wf_claim(C, q, 64, base);
+            if (n == 0) continue;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const bool mine = lane < n;
+            int s = -1, pixel = 0, sample = 0;
+            bool alive = false;
+            Path st;
+            if (mine) {
+                s = wf_take(ring[q], (base + (unsigned)lane) % (unsigned)NP);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample);
+                const float4 hh = r_h[s];
+                const Hit h{__float_as_int(hh.x), __float_as_int(hh.y), hh.z, hh.w, r_t[s], __float_as_int(hh.x) >= 0};
+                WfAov aov{A.albedo, A.normal, pixel, 1.0f / (float)(sample - P.first + 1)};
+                bool done;
+                if (SAMPLER == 1 && q == WF_LIGHT) done = light_hit<F>(S, P, st, h);
+                else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, h, aov, cnt.shades);
+                else done = path_hit<F>(S, P, st, h, aov, cnt.shades);
+                alive = true;
+                if (done) {
+                    finish(st, pixel, sample, aov);
+                    const int g = s >> 6;
+                    if (++sample < C.g_cs1[g]) {
+                        start_path(P, pixel % P.width, pixel / P.width, pixel, sample, st);
+                    } else {
+                        alive = false;
+                    }
+                }
+                if (alive) {
+                    wf_store<F>(recs + (size_t)s * RQ, st, pixel, sample);
+                    issue(s, st);
+                }
+            }
+            wf_push(C, ring[WF_TRAV], NP, WF_TRAV, alive, s);
+            // slots whose chunk is done: the last one of a group publishes the tile's running means
+            const bool fin = mine && !alive;
+            if (__builtin_amdgcn_ballot_w64(fin)) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                bool last = false;
+                int g = 0;
+                if (fin) {
+                    g = s >> 6;
+                    last = __hip_atomic_fetch_add(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 1;
+                }
+                if (__builtin_amdgcn_ballot_w64(last)) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    if (last) {
+                        if (C.g_uc[g] + 1 < nchunks)
+                            __hip_atomic_store(A.tile_done + C.g_tile[g], C.g_uc[g] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+            continue;
+        }
+
+        // ---------------------------------------------------------------- traverse
+        // refill: lanes without a query take the oldest waiting ones (first pop at once)
+        if (busy < 64 && tl > 0) {
+            const unsigned long long idle_m = ~busy_m;
+            unsigned base;
+            const int n = wf_claim(C, WF_TRAV, 64 - busy, base);
+            if (n > 0) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const int r = lane_rank(idle_m);
+                if (qslot < 0 && r < n) {
+                    const int s = wf_take(ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    const float4 o = q_o[s], d = q_d[s];
+                    const unsigned root = __float_as_uint(o.w);
+                    qslot = s | ((root >> 30) == T_INST ? 1 << 16 : 0);
+                    query_begin(T, V3(o.x, o.y, o.z), V3(d.x, d.y, d.z), root, stack);
+#pragma unroll
+                    for (int k = 0; k < JT_FIRST_POP; k++)
+                        if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
+                }
+            }
+        }
+        {
+            const bool wantp = T.nprim > 0;
+            const bool wantn = T.nprim == 0 && T.sp > 0;
+            const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
+            const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
+            if (np >= nn) {
+                if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+            } else {
+#pragma unroll
+                for (int k = 0; k < JT_NODE_REPEAT; k++)
+                    if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
+            }
+        }
+        // finished queries: the result to LDS, the slot onto its shading ring
+        const bool fin = qslot >= 0 && (T.sp | T.nprim) == 0;
+        if (__builtin_amdgcn_ballot_w64(fin)) {
+            const int s = qslot & 0xffff;
+            const bool light = (qslot >> 16) != 0;
+            if (fin) {
+                r_h[s] = make_float4(__int_as_float(T.h_inst), __int_as_float(T.h_elem), T.h_u, T.h_v);
+                r_t[s] = T.tmax;
+            }
+            wf_push(C, ring[WF_SCENE], NP, WF_SCENE, fin && !light, s);
+            wf_push(C, ring[WF_LIGHT], NP, WF_LIGHT, fin && light, s);
+            if (fin) qslot = -1;
+        }
+    }
+    unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
+                     COUNT ? cnt.shades : 0u};
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        unsigned sum = wave_sum(v[k]);
+        if (lane == 0 && sum) atomicAdd(&A.counters[k], (unsigned long long)sum);
+    }
+}
+
 // Occupancy request (waves per SIMD); JT_WAVES=0 leaves it to the compiler. The LDS-mode
 // FT_NONE kernel (cornellbox: 96 VGPRs, LDS for 5 workgroups per CU with the stack sized to the
 // scene) asks for JT_WAVES_NONE: measured +4 % over 4 waves with its wait_lanes of 56.
@@ -1206,6 +1667,38 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #define JT_WAVES_PER_EU
 #define JT_WAVES_PER_EU_F(F)
 #endif
+// WF kernels (trace_body_wf): occupancy request, 0 = the compiler's choice
+#ifndef JT_WAVES_WF
+#define JT_WAVES_WF 4
+#endif
+#if JT_WAVES_WF > 0
+#define JT_WAVES_PER_EU_WF __attribute__((amdgpu_waves_per_eu(JT_WAVES_WF, JT_WAVES_WF)))
+#else
+#define JT_WAVES_PER_EU_WF
+#endif
+
+// the scene arrays of the LDS blob (small-scene mode; offsets from jt_create)
+__device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob) {
+    DScene L = S;
+    L.nodes = reinterpret_cast<const DNode*>(blob + S.o_nodes);
+    L.tlas_prims = reinterpret_cast<const int*>(blob + S.o_tlas_prims);
+    L.prims = reinterpret_cast<const float4*>(blob + S.o_prims);
+    L.inst_trav = reinterpret_cast<const DInstTrav*>(blob + S.o_inst_trav);
+    L.inst_blas = reinterpret_cast<const int4*>(blob + S.o_inst_blas);
+    L.inst_shade = reinterpret_cast<const DInstShade*>(blob + S.o_inst_shade);
+    L.shapes = reinterpret_cast<const DShape*>(blob + S.o_shapes);
+    L.pos = reinterpret_cast<const float4*>(blob + S.o_pos);
+    L.nrm = reinterpret_cast<const float4*>(blob + S.o_nrm);
+    L.tc = reinterpret_cast<const float2*>(blob + S.o_tc);
+    L.col = reinterpret_cast<const float4*>(blob + S.o_col);
+    L.elems = reinterpret_cast<const int4*>(blob + S.o_elems);
+    L.enrm = reinterpret_cast<const float4*>(blob + S.o_enrm);
+    L.enrm_id = reinterpret_cast<const float4*>(blob + S.o_enrm_id);
+    L.materials = reinterpret_cast<const DMaterial*>(blob + S.o_materials);
+    L.lights = reinterpret_cast<const DLight*>(blob + S.o_lights);
+    L.cdf = reinterpret_cast<const float*>(blob + S.o_cdf);
+    return L;
+}
 
 // HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS. The
 // workgroup first copies the top nlnodes nodes (the breadth-first top of the TLAS, visited by
@@ -1232,25 +1725,28 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(D
     uint4* blob = dyn_lds + ((OVF ? RING : S.stack_need) * BLOCK) / 4;  // the stack takes the first entries
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
-    DScene L = S;
-    L.nodes = reinterpret_cast<const DNode*>(blob + S.o_nodes);
-    L.tlas_prims = reinterpret_cast<const int*>(blob + S.o_tlas_prims);
-    L.prims = reinterpret_cast<const float4*>(blob + S.o_prims);
-    L.inst_trav = reinterpret_cast<const DInstTrav*>(blob + S.o_inst_trav);
-    L.inst_blas = reinterpret_cast<const int4*>(blob + S.o_inst_blas);
-    L.inst_shade = reinterpret_cast<const DInstShade*>(blob + S.o_inst_shade);
-    L.shapes = reinterpret_cast<const DShape*>(blob + S.o_shapes);
-    L.pos = reinterpret_cast<const float4*>(blob + S.o_pos);
-    L.nrm = reinterpret_cast<const float4*>(blob + S.o_nrm);
-    L.tc = reinterpret_cast<const float2*>(blob + S.o_tc);
-    L.col = reinterpret_cast<const float4*>(blob + S.o_col);
-    L.elems = reinterpret_cast<const int4*>(blob + S.o_elems);
-    L.enrm = reinterpret_cast<const float4*>(blob + S.o_enrm);
-    L.enrm_id = reinterpret_cast<const float4*>(blob + S.o_enrm_id);
-    L.materials = reinterpret_cast<const DMaterial*>(blob + S.o_materials);
-    L.lights = reinterpret_cast<const DLight*>(blob + S.o_lights);
-    L.cdf = reinterpret_cast<const float*>(blob + S.o_cdf);
+    const DScene L = blob_scene(S, blob);
     trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+}
+
+// WF kernels (trace_body_wf, stack bound <= 16): dynamic LDS = the lanes' stacks, the WF rings /
+// queries / results, then the scene blob (LDS mode) or nothing (HBM mode: the scene from L2).
+template <int SAMPLER, int COUNT, int F, bool LDSM>
+__global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_WF void trace_kernel_wf(DScene S, DParams P, int s_begin, int s_end,
+                                                                            DAccum A, float4* pool) {
+    extern __shared__ uint4 dyn_lds[];
+    const int NP = 64 * P.wf_groups;
+    int* const stack = reinterpret_cast<int*>(dyn_lds);
+    int* const wf = stack + S.stack_need * BLOCK;
+    uint4* const blob = reinterpret_cast<uint4*>(wf + 3 * NP) + 3 * NP + NP / 4;
+    DScene L = S;
+    if (LDSM) {
+        for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
+        __syncthreads();
+        L = blob_scene(S, blob);
+    }
+    L.nlnodes = 0;
+    trace_body_wf<SAMPLER, COUNT, F, !LDSM>(L, P, s_begin, s_end, A, stack + threadIdx.x, wf, pool);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of
@@ -1279,6 +1775,29 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, cache) != hipSuccess || per_cu < 1) per_cu = 1;
     const int nwg = std::min(want, per_cu * cus);
     hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), cache, st, S, P, s0, s1, A);
+    return hipGetLastError();
+}
+
+// WF launch (trace_body_wf): every resident workgroup, each with wf_groups * 64 path slots
+template <int SAMPLER, int COUNT, int F>
+hipError_t launch_wf(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
+    const int NP = 64 * P.wf_groups;
+    const bool ldsm = S.blob_n16 > 0;
+    const size_t lds = (size_t)S.stack_need * BLOCK * 4 + (size_t)NP * (3 * 4 + 3 * 16 + 4) +
+                       (ldsm ? (size_t)S.blob_n16 * 16 : 0);
+    const void* k = ldsm ? (const void*)trace_kernel_wf<SAMPLER, COUNT, F, true>
+                         : (const void*)trace_kernel_wf<SAMPLER, COUNT, F, false>;
+    hipError_t e;
+    if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    const size_t rec = (size_t)NP * wf_rec_q(F) * 16;
+    const int nwg = (int)std::min<size_t>((size_t)per_cu * cus, A.pool_bytes / rec);
+    if (nwg < 1) return hipErrorInvalidValue;
+    if (ldsm)
+        hipLaunchKernelGGL((trace_kernel_wf<SAMPLER, COUNT, F, true>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A, A.pool);
+    else
+        hipLaunchKernelGGL((trace_kernel_wf<SAMPLER, COUNT, F, false>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A, A.pool);
     return hipGetLastError();
 }
 
@@ -1311,6 +1830,10 @@ hipError_t launch_s(int need, int ring, int kmask, const DScene& S, const DParam
     return launch_t<1, 16, false, 0, JT_ONE_FEAT>(S, P, s0, s1, A, st, cus);
 #else
     if (need <= 16) {
+        if (P.wf_groups > 0) {
+            if (kmask == FT_NONE) return launch_wf<SAMPLER, COUNT, FT_NONE>(S, P, s0, s1, A, st, cus);
+            return launch_wf<SAMPLER, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
+        }
         if (kmask == FT_NONE) return launch_t<SAMPLER, 16, false, COUNT, FT_NONE>(S, P, s0, s1, A, st, cus);
         return launch_t<SAMPLER, 16, false, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
     }
@@ -1984,6 +2507,16 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
     P.light_lanes = 2;
     if (const char* ll = std::getenv("JT_LIGHT_LANES")) P.light_lanes = std::max(1, std::min(65, std::atoi(ll)));
+    // WF body (trace_body_wf): scenes whose stack bound fits the lanes' 16-entry LDS stacks
+    P.wf_groups = 0;
+    if (const char* wf = std::getenv("JT_WF")) {
+        if (std::atoi(wf) > 0 && c->stack <= 16) {
+            P.wf_groups = 6;
+            if (const char* g = std::getenv("JT_WF_GROUPS")) P.wf_groups = std::max(1, std::min(WF_GMAX, std::atoi(g)));
+            P.wait_lanes = 56;
+            if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
+        }
+    }
 
     // accumulators (make_trace_state: zeroed) + counters
     const size_t np = (size_t)W * (size_t)H;
@@ -2007,7 +2540,15 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, params->device) == hipSuccess && cus > 0) c->cus = cus;
     c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt,
-                  (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE};
+                  (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE, nullptr, 0};
+    if (P.wf_groups > 0) {  // path-slot records: at most 8 workgroups of 256 lanes per CU
+        const size_t bytes = (size_t)c->cus * 8 * 64 * WF_GMAX * wf_rec_q(FT_ALL) * 16;
+        void* pool = nullptr;
+        if ((e = hipMalloc(&pool, bytes)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc WF path records"));
+        c->allocations.push_back(pool);
+        c->A.pool = (float4*)pool;
+        c->A.pool_bytes = bytes;
+    }
     st = jt_reset(c);
     if (st != JT_OK) return bail(st);
     *out = c;
@@ -2175,10 +2716,10 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     char tmp[512];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d light_lanes=%d chunk=%d tiles=%d block=%d",
-                  c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
+                  "wait_lanes=%d light_lanes=%d chunk=%d tiles=%d block=%d wf_groups=%d",
+                  c->P.wf_groups ? "trace_kernel_wf" : c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, c->kmask, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
-                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->tiles, BLOCK);
+                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->tiles, BLOCK, c->P.wf_groups);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;
 }

@@ -1,0 +1,17 @@
+# WF body: bitwise tests against the megakernel body, then bench sweeps (experiment launcher)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/$1
+mkdir -p $O
+scripts/gpu_step.sh 300 $O/pytest_wf.log timeout -k 10 280 python -u -m pytest tests/test_gpu_wf.py -x -v --timeout 60 --timeout-method thread || exit 1
+grep -q " passed" $O/pytest_wf.log || exit 1
+grep -q "failed" $O/pytest_wf.log && exit 1
+scripts/gpu_step.sh 120 $O/bench_mk.log timeout -k 10 100 python bench.py --no-cpu-baseline --steps 2 || exit 1
+for g in 5 6; do for wl in 40 56 64; do
+  JT_WF=1 JT_WF_GROUPS=$g JT_WAIT_LANES=$wl scripts/gpu_step.sh 120 $O/bench_wf_g${g}_w${wl}.log timeout -k 10 100 python bench.py --no-cpu-baseline --steps 2 || exit 1
+done; done
+grep -h '"value"' $O/bench_*.log | python -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); print(d['value'], d['roofline']['launch'][:40], d['roofline']['launch'].split('wait_lanes=')[1].split()[0], d['roofline']['launch'].split('wf_groups=')[1])"
