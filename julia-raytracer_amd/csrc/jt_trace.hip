@@ -1242,6 +1242,7 @@ struct WfCtl {
     int g_left[WF_GMAX];  // -1 idle, -2 unit assigned and waiting for its tile's previous chunk, >= 0 slots running
     int band_k;
     int exhausted;        // every band's units handed out
+    int abort;            // a ring entry never arrived (never expected): every wave leaves, the launch fails
 };
 __host__ __device__ constexpr int wf_rec_q(int F) { return (F & FT_VOL) ? 10 : 8; }  // float4s per slot record
 
@@ -1319,9 +1320,17 @@ __device__ __forceinline__ int wf_claim(WfCtl& C, int q, int want, unsigned& bas
     return __builtin_amdgcn_readfirstlane(n);
 }
 // entry `idx` of a ring: its producer reserved it before writing it, so wait for the write
-__device__ __forceinline__ int wf_take(int* ring, unsigned idx) {
+// (bounded: a missing entry aborts the launch instead of hanging the GPU)
+__device__ __forceinline__ int wf_take(WfCtl& C, int* ring, unsigned idx) {
     int s;
-    while ((s = __hip_atomic_load(ring + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) __builtin_amdgcn_s_sleep(1);
+    unsigned n = 0;
+    while ((s = __hip_atomic_load(ring + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++n > (1u << 22)) {
+            __hip_atomic_store(&C.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return 0;
+        }
+    }
     __hip_atomic_store(ring + idx, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return s;
 }
@@ -1360,6 +1369,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     if (threadIdx.x == 0) {
         C.band_k = 0;
         C.exhausted = 0;
+        C.abort = 0;
     }
     for (int k = threadIdx.x; k < 3 * NP; k += BLOCK) lds_wf[k] = -1;
     __syncthreads();
@@ -1459,6 +1469,10 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             job = __builtin_amdgcn_readfirstlane((int)done) ? 4 : 5;
         }
         if (job == 4) break;
+        if (__hip_atomic_load(&C.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            if (lane == 0) atomicAdd(A.counters + 7, 1ull);
+            break;
+        }
         if (job == 5) {  // other waves hold this workgroup's last queries / a tile wait: bounded wait
             __builtin_amdgcn_s_sleep(4);
             if (++idle_iters > (1u << 26)) {
@@ -1525,9 +1539,8 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                 wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0);
                 issue(s, st);
             }
-            if (lane == 0)
-                __hip_atomic_store(&C.g_left[g], lane_count(__builtin_amdgcn_ballot_w64(in_image)), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int started = lane_count(__builtin_amdgcn_ballot_w64(in_image));
+            if (lane == 0) __hip_atomic_store(&C.g_left[g], started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             wf_push(C, ring[WF_TRAV], NP, WF_TRAV, in_image, s);
             continue;
         }
@@ -1544,7 +1557,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             bool alive = false;
             Path st;
             if (mine) {
-                s = wf_take(ring[q], (base + (unsigned)lane) % (unsigned)NP);
+                s = wf_take(C, ring[q], (base + (unsigned)lane) % (unsigned)NP);
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample);
                 const float4 hh = r_h[s];
@@ -1602,7 +1615,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 const int r = lane_rank(idle_m);
                 if (qslot < 0 && r < n) {
-                    const int s = wf_take(ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
+                    const int s = wf_take(C, ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                     const float4 o = q_o[s], d = q_d[s];
                     const unsigned root = __float_as_uint(o.w);
