@@ -156,6 +156,7 @@ struct DParams {
                       // many lanes wait on a sample_lights_pdf query result (65: never)
     int chunk;  // samples per work unit (a tile's chunks run in order)
     int wf_groups;  // WF body: 64-slot path groups per workgroup
+    int wf_refill;  // WF body: idle lanes that make a traversal step first take new queries
     unsigned long long seed;
 };
 

@@ -671,32 +671,6 @@ __device__ __forceinline__ void aov_update(const Aov& a, v3 ta, v3 tn) {
     p[9 * BLOCK] = p[9 * BLOCK] * omw + tn.z * aw;
 }
 
-// The WF body's accessor (trace_body_wf): the pixel's albedo / normal running means are read-
-// modified-written in HBM (each pixel has one owning path slot, whose samples run in order),
-// with the same float operations as aov_update's LDS form.
-struct WfAov {
-    float4* albedo;
-    float4* normal;
-    int pixel;
-    float w_;
-    template <int F>
-    __device__ __forceinline__ float w() const { return w_; }
-};
-template <int F>
-__device__ __forceinline__ void aov_update(const WfAov& a, v3 ta, v3 tn) {
-    const float aw = a.w_;
-    const float omw = 1 - aw;
-    float4 al = a.albedo[a.pixel], nr = a.normal[a.pixel];
-    al.x = al.x * omw + ta.x * aw;
-    al.y = al.y * omw + ta.y * aw;
-    al.z = al.z * omw + ta.z * aw;
-    nr.x = nr.x * omw + tn.x * aw;
-    nr.y = nr.y * omw + tn.y * aw;
-    nr.z = nr.z * omw + tn.z * aw;
-    a.albedo[a.pixel] = al;
-    a.normal[a.pixel] = nr;
-}
-
 template <int F, class AovT>
 __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const AovT& aov,
                                          unsigned& shades) {
@@ -1219,35 +1193,43 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 
 // ============================================================================ WF body
 // trace_samples with the queries decoupled from the paths (DESIGN.md §2 "WF scheduling"). A
-// workgroup owns P = 64 * G path slots, G slot groups of one 8x8 tile x sample chunk each (more
-// paths than its 256 lanes). A slot's path state lives in a 128/160-B record in HBM (L2) between
-// shading steps; its pending BVH query (origin, direction, root) in LDS. Three LDS rings hold
-// slot ids: queries waiting for a lane, scene results and light results waiting for shading.
-// Every iteration each wave picks one wave-uniform job:
-//   - start an idle group on a new work unit (64 new paths, one per lane);
-//   - shade a batch of up to 64 waiting results (scene or light ring): load the slot's path,
-//     path_hit / naive_hit / light_hit, issue its next query or finish its sample;
-//   - traverse: lanes without a query take one from the ring, then one node/primitive step kind.
-// A lane's query runs on that lane to completion (its stack is the lane's LDS stack), but any
-// lane may run any slot's query, and any wave may shade any slot: traversal steps run on nearly
-// full waves and shading steps on full batches, instead of the idle lanes a per-lane path
-// leaves while it waits. Each path's float operations and RNG draws are the reference's, in its
-// order, and a pixel's samples are accumulated in order (one slot per pixel and chunk; chunks of
-// a tile in order, as trace_body): results are bit-identical to trace_body.
+// workgroup owns NP = 64 * G path slots: G slot groups, each one 8x8 tile x sample chunk (more
+// paths than its 256 lanes). Between shading steps a slot's path state and its pixel's running
+// means live in a record in HBM (L2); its pending BVH query (origin, direction, root) in LDS.
+// Three LDS rings hold slot ids: queries waiting for a lane, scene results and light results
+// waiting for shading. Each wave repeatedly picks one wave-uniform job:
+//   - start a slot group on a new work unit (64 new paths, one per lane);
+//   - shade a batch of up to 64 waiting results (scene or light ring): load the slot record,
+//     path_hit / naive_hit / light_hit, then issue the slot's next query or finish its sample;
+//   - traverse for a few iterations: lanes without a query take one from the ring, then one
+//     node/primitive step kind (the megakernel's step code).
+// A query runs on one lane to completion (its stack is that lane's LDS stack), but any lane may
+// run any slot's query and any wave may shade any slot: traversal runs on nearly full waves and
+// shading on full batches. Each path's float operations and RNG draws are the reference's, in
+// its order, and a pixel's samples are accumulated in order (one slot per pixel and chunk; the
+// chunks of a tile in order): results are bit-identical to trace_body.
 constexpr int WF_GMAX = 8;
 constexpr int WF_TRAV = 0, WF_SCENE = 1, WF_LIGHT = 2;
 struct WfCtl {
-    unsigned head[3], tail[3];
+    unsigned head[3], tail[3];  // ring cursors
+    unsigned attn;              // groups a wave should look at: idle while units remain, or waiting on a tile
+    unsigned live;              // groups holding (or claiming) a unit
     int g_tile[WF_GMAX], g_uc[WF_GMAX], g_cs1[WF_GMAX];
-    int g_left[WF_GMAX];  // -1 idle, -2 unit assigned and waiting for its tile's previous chunk, >= 0 slots running
+    int g_left[WF_GMAX];  // -1 idle, -2 waiting for the tile's previous chunk, -3/-4 claimed, >= 0 slots running
     int band_k;
-    int exhausted;        // every band's units handed out
-    int abort;            // a ring entry never arrived (never expected): every wave leaves, the launch fails
+    int exhausted;  // every band's units handed out
+    int abort;      // a ring entry never arrived (never expected): every wave leaves, the launch fails
 };
-__host__ __device__ constexpr int wf_rec_q(int F) { return (F & FT_VOL) ? 10 : 8; }  // float4s per slot record
-
+// float4s per slot record: path state (8), running means (3), the volume (2, FT_VOL)
+__host__ __device__ constexpr int wf_rec_q(int F) { return (F & FT_VOL) ? 13 : 11; }
+struct WfAcc {  // a slot's pixel running means (trace_body's acc slots), in registers while it shades
+    float4 im;
+    v3 al, nr;
+    int hits;
+    float w;
+};
 template <int F>
-__device__ __forceinline__ void wf_store(float4* r, const Path& st, int pixel, int sample) {
+__device__ __forceinline__ void wf_store(float4* r, const Path& st, int pixel, int sample, const WfAcc& a) {
     const unsigned long long s = st.rng.state, c = st.rng.inc;
     r[0] = make_float4(st.o.x, st.o.y, st.o.z, st.d.x);
     r[1] = make_float4(st.d.y, st.d.z, st.radiance.x, st.radiance.y);
@@ -1258,53 +1240,86 @@ __device__ __forceinline__ void wf_store(float4* r, const Path& st, int pixel, i
                        st.max_roughness);
     r[5] = make_float4(__int_as_float(st.li), __int_as_float(st.lcount), st.pb, st.pdf);
     r[6] = make_float4(st.lpdf, st.lq.x, st.lq.y, st.lq.z);
-    r[7] = make_float4(__int_as_float(pixel), __int_as_float(sample), 0.0f, 0.0f);
+    r[7] = make_float4(__int_as_float(pixel), __int_as_float(sample), a.w, __int_as_float(a.hits));
+    r[8] = a.im;
+    r[9] = make_float4(a.al.x, a.al.y, a.al.z, a.nr.x);
+    r[10] = make_float4(a.nr.y, a.nr.z, 0.0f, 0.0f);
     if (F & FT_VOL) {
-        r[8] = make_float4(st.vol.density.x, st.vol.density.y, st.vol.density.z, st.vol.scattering.x);
-        r[9] = make_float4(st.vol.scattering.y, st.vol.scattering.z, st.vol.scanisotropy, 0.0f);
+        r[11] = make_float4(st.vol.density.x, st.vol.density.y, st.vol.density.z, st.vol.scattering.x);
+        r[12] = make_float4(st.vol.scattering.y, st.vol.scattering.z, st.vol.scanisotropy, 0.0f);
     }
 }
 template <int F>
-__device__ __forceinline__ void wf_load(const float4* r, Path& st, int& pixel, int& sample) {
-    const float4 a = r[0], b = r[1], c = r[2], d = r[3], e = r[4], f = r[5], g = r[6], h = r[7];
-    st.o = V3(a.x, a.y, a.z);
-    st.d = V3(a.w, b.x, b.y);
-    st.radiance = V3(b.z, b.w, c.x);
-    st.weight = V3(c.y, c.z, c.w);
-    st.rng.state = (unsigned long long)__float_as_uint(d.x) | (unsigned long long)__float_as_uint(d.y) << 32;
-    st.rng.inc = (unsigned long long)__float_as_uint(d.z) | (unsigned long long)__float_as_uint(d.w) << 32;
-    st.bounce = __float_as_int(e.x);
-    st.opbounce = __float_as_int(e.y);
-    st.flags = __float_as_int(e.z) & 0xff;
-    st.phase = __float_as_int(e.z) >> 8;
-    st.max_roughness = e.w;
-    st.li = __float_as_int(f.x);
-    st.lcount = __float_as_int(f.y);
-    st.pb = f.z;
-    st.pdf = f.w;
-    st.lpdf = g.x;
-    st.lq = V3(g.y, g.z, g.w);
-    pixel = __float_as_int(h.x);
-    sample = __float_as_int(h.y);
+__device__ __forceinline__ void wf_load(const float4* r, Path& st, int& pixel, int& sample, WfAcc& a) {
+    const float4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6], q7 = r[7];
+    const float4 q8 = r[8], q9 = r[9], q10 = r[10];
+    st.o = V3(q0.x, q0.y, q0.z);
+    st.d = V3(q0.w, q1.x, q1.y);
+    st.radiance = V3(q1.z, q1.w, q2.x);
+    st.weight = V3(q2.y, q2.z, q2.w);
+    st.rng.state = (unsigned long long)__float_as_uint(q3.x) | (unsigned long long)__float_as_uint(q3.y) << 32;
+    st.rng.inc = (unsigned long long)__float_as_uint(q3.z) | (unsigned long long)__float_as_uint(q3.w) << 32;
+    st.bounce = __float_as_int(q4.x);
+    st.opbounce = __float_as_int(q4.y);
+    st.flags = __float_as_int(q4.z) & 0xff;
+    st.phase = __float_as_int(q4.z) >> 8;
+    st.max_roughness = q4.w;
+    st.li = __float_as_int(q5.x);
+    st.lcount = __float_as_int(q5.y);
+    st.pb = q5.z;
+    st.pdf = q5.w;
+    st.lpdf = q6.x;
+    st.lq = V3(q6.y, q6.z, q6.w);
+    pixel = __float_as_int(q7.x);
+    sample = __float_as_int(q7.y);
+    a.w = q7.z;
+    a.hits = __float_as_int(q7.w);
+    a.im = q8;
+    a.al = V3(q9.x, q9.y, q9.z);
+    a.nr = V3(q9.w, q10.x, q10.y);
     if (F & FT_VOL) {
-        const float4 v0 = r[8], v1 = r[9];
+        const float4 v0 = r[11], v1 = r[12];
         st.vol.density = V3(v0.x, v0.y, v0.z);
         st.vol.scattering = V3(v0.w, v1.x, v1.y);
         st.vol.scanisotropy = v1.z;
     }
 }
 
+// the WF body's AOV accessor: the slot's running means in registers (same float operations as
+// aov_update's LDS form)
+struct WfAov {
+    WfAcc* acc;
+    template <int F>
+    __device__ __forceinline__ float w() const { return acc->w; }
+};
+template <int F>
+__device__ __forceinline__ void aov_update(const WfAov& a, v3 ta, v3 tn) {
+    WfAcc& c = *a.acc;
+    const float aw = c.w;
+    const float omw = 1 - aw;
+    c.al = V3(c.al.x * omw + ta.x * aw, c.al.y * omw + ta.y * aw, c.al.z * omw + ta.z * aw);
+    c.nr = V3(c.nr.x * omw + tn.x * aw, c.nr.y * omw + tn.y * aw, c.nr.z * omw + tn.z * aw);
+}
+
 __device__ __forceinline__ int lane_rank(unsigned long long m) {  // active lanes of m below this lane
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
-// claim up to `want` entries of ring q (wave-uniform result); the entries are then read with wf_take
+__device__ __forceinline__ unsigned lds_ld(const unsigned* a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int lds_ld(const int* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// LDS writes issued before this point reach LDS before any later LDS access of this wave, and
+// the compiler keeps them in order (a wave's LDS operations execute in issue order)
+__device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// claim up to `want` entries of ring q (wave-uniform count); read them with wf_take
 __device__ __forceinline__ int wf_claim(WfCtl& C, int q, int want, unsigned& base) {
     unsigned h = 0;
     int n = 0;
     if ((threadIdx.x & 63) == 0) {
         for (;;) {
-            h = __hip_atomic_load(&C.head[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const unsigned t = __hip_atomic_load(&C.tail[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            h = lds_ld(&C.head[q]);
+            const unsigned t = lds_ld(&C.tail[q]);
             n = (int)(t - h) < want ? (int)(t - h) : want;
             if (n <= 0) {
                 n = 0;
@@ -1334,19 +1349,22 @@ __device__ __forceinline__ int wf_take(WfCtl& C, int* ring, unsigned idx) {
     __hip_atomic_store(ring + idx, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return s;
 }
-// push this lane's slot onto ring q when `pred`; everything the consumer reads (LDS query / result,
-// the HBM record) was written before: workgroup-scope release first
-__device__ __forceinline__ void wf_push(WfCtl& C, int* ring, int P, int q, bool pred, int slot) {
+// push this lane's slot onto ring q when `pred`; the caller has ordered what the consumer reads
+// (lds_order for LDS data, a workgroup release fence for the HBM record) before this
+__device__ __forceinline__ void wf_push(WfCtl& C, int* ring, int NP, int q, bool pred, int slot) {
     const unsigned long long m = __builtin_amdgcn_ballot_w64(pred);
     if (!m) return;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     unsigned base = 0;
     if ((threadIdx.x & 63) == 0) base = __hip_atomic_fetch_add(&C.tail[q], (unsigned)lane_count(m), __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_WORKGROUP);
     base = __builtin_amdgcn_readfirstlane(base);
-    if (pred) __hip_atomic_store(ring + (base + (unsigned)lane_rank(m)) % (unsigned)P, slot, __ATOMIC_RELAXED,
+    if (pred) __hip_atomic_store(ring + (base + (unsigned)lane_rank(m)) % (unsigned)NP, slot, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+
+#ifndef JT_WF_TRAV_ITERS
+#define JT_WF_TRAV_ITERS 8
+#endif
 
 template <int SAMPLER, int COUNT, int F, bool NCACHE>
 __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A, int* stack,
@@ -1367,6 +1385,8 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     }
     if (threadIdx.x < WF_GMAX) C.g_left[threadIdx.x] = -1;
     if (threadIdx.x == 0) {
+        C.attn = (1u << G) - 1;
+        C.live = 0;
         C.band_k = 0;
         C.exhausted = 0;
         C.abort = 0;
@@ -1383,9 +1403,10 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     T.sp = 0;
     T.nprim = 0;
     int qslot = -1;  // the slot whose query this lane runs (-1: none); bit 16: a light query
+    int pend = -1;   // a slot this lane shaded whose next query waits to be pushed (after its record store)
     unsigned idle_iters = 0;
 
-    // a slot's pending query: written to LDS, then its id pushed onto the traversal ring
+    // a slot's pending query (LDS): origin, direction, root
     auto issue = [&](int s, const Path& st) {
         const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
         const v3 o = light ? st.lq : st.o;
@@ -1396,86 +1417,64 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
         if (light) cnt.light_queries++;
         else cnt.rays++;
     };
-    // trace_sample's epilogue (src/trace.jl:625-648) for the slot's pixel: HBM read-modify-write
-    auto finish = [&](Path& st, int pixel, int sample, const WfAov& aov) {
-        cnt.paths++;
-        v3 radiance = st.radiance;
-        if (!all_finite(radiance)) radiance = V3(0, 0, 0);
-        const float mr = max3(radiance);
-        if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
-        const float w = aov.w_;
-        const float omw = 1 - w;
-        const bool hit = st.flags & F_HIT;
-        const bool env = !hit && !P.envhidden && S.nenvs != 0;
-        const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
-        if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
-        float4 im = A.image[pixel];
-        im.x = im.x * omw + target.x * w;
-        im.y = im.y * omw + target.y * w;
-        im.z = im.z * omw + target.z * w;
-        im.w = im.w * omw + target.w * w;
-        A.image[pixel] = im;
-        if (hit || env) A.hits[pixel] += 1;
-        (void)sample;
-    };
 
     for (;;) {
+        // queries issued by the last shading job: their records are stored, now publish them
+        if (__builtin_amdgcn_ballot_w64(pend >= 0)) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            wf_push(C, ring[WF_TRAV], NP, WF_TRAV, pend >= 0, pend);
+            pend = -1;
+        }
+        if (lds_ld(&C.abort)) {
+            if (lane == 0) atomicAdd(A.counters + 7, 1ull);
+            break;
+        }
         // ---------------------------------------------------------------- pick the wave's job
-        int job = 0;        // 0 traverse, 1 start group, 2 shade scene ring, 3 shade light ring, 4 exit, 5 idle
+        // the control words, one per lane (one LDS round trip)
+        const unsigned cv = lane < 8 ? lds_ld(reinterpret_cast<const unsigned*>(&C) + lane) : 0u;
+        const unsigned tl = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
+        const unsigned sl = __builtin_amdgcn_readlane(cv, 4) - __builtin_amdgcn_readlane(cv, 1);
+        const unsigned ll = __builtin_amdgcn_readlane(cv, 5) - __builtin_amdgcn_readlane(cv, 2);
+        const unsigned attn = __builtin_amdgcn_readlane(cv, 6);
+        int busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
         int gsel = -1;
-        unsigned tl = 0, sl = 0, ll = 0;
-        const unsigned long long busy_m = __builtin_amdgcn_ballot_w64(qslot >= 0);
-        const int busy = lane_count(busy_m);
-        auto ld = [](unsigned* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-        const bool exhausted = __hip_atomic_load(&C.exhausted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-        if (lane == 0) {
-            tl = ld(&C.tail[0]) - ld(&C.head[0]);
-            sl = ld(&C.tail[1]) - ld(&C.head[1]);
-            ll = ld(&C.tail[2]) - ld(&C.head[2]);
-            // a group waiting for its tile's previous chunk, or an idle group while units remain
-            for (int g = 0; g < G && gsel < 0; g++) {
-                const int gl = __hip_atomic_load(&C.g_left[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (gl == -2) {
-                    if (__hip_atomic_load(A.tile_done + C.g_tile[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= C.g_uc[g]) {
-                        int expect = -2;
-                        if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+        if (attn) {  // a group to start: an idle one while units remain, or one whose tile is ready
+            if (lane == 0) {
+                for (int g = 0; g < G && gsel < 0; g++) {
+                    if (!((attn >> g) & 1)) continue;
+                    const int gl = lds_ld(&C.g_left[g]);
+                    int expect = gl;
+                    if (gl == -2) {
+                        if (__hip_atomic_load(A.tile_done + C.g_tile[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= C.g_uc[g] &&
+                            __hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_WORKGROUP))
                             gsel = g;
+                    } else if (gl == -1) {
+                        if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -4, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                            gsel = g;
+                            __hip_atomic_fetch_add(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
                     }
-                } else if (gl == -1 && !exhausted) {
-                    int expect = -1;
-                    if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -4, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP))
-                        gsel = g;
+                    if (gsel >= 0) __hip_atomic_fetch_and(&C.attn, ~(1u << g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
+            gsel = __builtin_amdgcn_readfirstlane(gsel);
         }
-        gsel = __builtin_amdgcn_readfirstlane(gsel);
-        tl = __builtin_amdgcn_readfirstlane(tl);
-        sl = __builtin_amdgcn_readfirstlane(sl);
-        ll = __builtin_amdgcn_readfirstlane(ll);
         const unsigned qmax = sl > ll ? sl : ll;
+        int job;  // 0 traverse, 1 start group, 2 shade scene ring, 3 shade light ring, 5 nothing to do
         if (gsel >= 0) job = 1;
         else if (qmax >= (unsigned)P.wait_lanes || (qmax > 0 && tl == 0 && (unsigned)busy < qmax)) job = sl >= ll ? 2 : 3;
         else if (busy > 0 || tl > 0) job = 0;
         else if (qmax > 0) job = sl >= ll ? 2 : 3;
-        else {
-            bool done = false;
-            if (lane == 0) {
-                done = exhausted;
-                for (int g = 0; g < G; g++)
-                    done = done && __hip_atomic_load(&C.g_left[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == -1;
-            }
-            job = __builtin_amdgcn_readfirstlane((int)done) ? 4 : 5;
-        }
-        if (job == 4) break;
-        if (__hip_atomic_load(&C.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            if (lane == 0) atomicAdd(A.counters + 7, 1ull);
-            break;
-        }
-        if (job == 5) {  // other waves hold this workgroup's last queries / a tile wait: bounded wait
+        else job = 5;
+
+        if (job == 5) {
+            // nothing here: the workgroup is done, or other waves hold its last queries / a tile wait
+            const bool done = lds_ld(&C.exhausted) && lds_ld(&C.live) == 0u;
+            if (done) break;
             __builtin_amdgcn_s_sleep(4);
-            if (++idle_iters > (1u << 26)) {
+            if (++idle_iters > (1u << 26)) {  // bounded: never expected
                 if (lane == 0) atomicAdd(A.counters + 7, 1ull);
                 break;
             }
@@ -1485,15 +1484,14 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
 
         if (job == 1) {
             // ------------------------------------------------------------ start a slot group
-            int g = gsel;
-            int claimed_left = 0;
-            if (lane == 0) claimed_left = C.g_left[g];
-            claimed_left = __builtin_amdgcn_readfirstlane(claimed_left);
-            if (claimed_left == -4) {  // idle group: fetch a unit (XCD band first, then the others)
-                int unit_uc = -1, unit_t = 0;
-                if (lane == 0) {
+            const int g = gsel;
+            int state = 0;
+            if (lane == 0) {
+                state = C.g_left[g];
+                if (state == -4) {  // idle group: fetch a unit (this XCD's band first, then the others)
+                    int unit_uc = -1, unit_t = 0;
                     for (;;) {
-                        const int bk = __hip_atomic_load(&C.band_k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        const int bk = lds_ld(&C.band_k);
                         if (bk >= NBANDS) break;
                         const int band = (int)((xcc + (unsigned)bk) & (NBANDS - 1));
                         const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
@@ -1507,25 +1505,29 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                         __hip_atomic_compare_exchange_strong(&C.band_k, &expect, bk + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                              __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    if (unit_uc < 0) {
+                    if (unit_uc < 0) {  // no units left: this group stays idle
                         __hip_atomic_store(&C.exhausted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_sub(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        state = -1;
                     } else {
                         C.g_tile[g] = unit_t;
                         C.g_uc[g] = unit_uc;
                         const int cs0 = s_begin + unit_uc * P.chunk;
                         C.g_cs1[g] = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
-                        if (unit_uc > 0 && __hip_atomic_load(A.tile_done + unit_t, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT) < unit_uc) {
+                        if (unit_uc > 0 &&
+                            __hip_atomic_load(A.tile_done + unit_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unit_uc) {
+                            // its tile's previous chunk is not published yet: start it later
                             __hip_atomic_store(&C.g_left[g], -2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            unit_uc = -2;  // started later, when the previous chunk is published
+                            __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            state = -2;
                         }
                     }
                 }
-                unit_uc = __builtin_amdgcn_readfirstlane(unit_uc);
-                if (unit_uc < 0) continue;
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            state = __builtin_amdgcn_readfirstlane(state);
+            if (state == -1 || state == -2) continue;
+            lds_order();
             const int ut = C.g_tile[g], uc = C.g_uc[g];
             if (uc > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's running means
             const int i = (ut % tiles_x) * 8 + (lane & 7), j = (ut / tiles_x) * 8 + (lane >> 3);
@@ -1534,14 +1536,16 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             const int cs0 = s_begin + uc * P.chunk;
             const int pixel = j * P.width + i;
             if (in_image) {
+                const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
+                WfAcc acc{im, V3(al.x, al.y, al.z), V3(nr.x, nr.y, nr.z), 0, 1.0f / (float)(cs0 - P.first + 1)};
                 Path st;
                 start_path(P, i, j, pixel, cs0, st);
-                wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0);
+                wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0, acc);
                 issue(s, st);
+                pend = s;
             }
             const int started = lane_count(__builtin_amdgcn_ballot_w64(in_image));
             if (lane == 0) __hip_atomic_store(&C.g_left[g], started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            wf_push(C, ring[WF_TRAV], NP, WF_TRAV, in_image, s);
             continue;
         }
 
@@ -1551,54 +1555,75 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             unsigned base;
             const int n = wf_claim(C, q, 64, base);
             if (n == 0) continue;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             const bool mine = lane < n;
-            int s = -1, pixel = 0, sample = 0;
+            int s = -1;
             bool alive = false;
-            Path st;
             if (mine) {
                 s = wf_take(C, ring[q], (base + (unsigned)lane) % (unsigned)NP);
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample);
+                Path st;
+                WfAcc acc;
+                int pixel, sample;
+                wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
                 const float4 hh = r_h[s];
                 const Hit h{__float_as_int(hh.x), __float_as_int(hh.y), hh.z, hh.w, r_t[s], __float_as_int(hh.x) >= 0};
-                WfAov aov{A.albedo, A.normal, pixel, 1.0f / (float)(sample - P.first + 1)};
+                const WfAov aov{&acc};
                 bool done;
                 if (SAMPLER == 1 && q == WF_LIGHT) done = light_hit<F>(S, P, st, h);
                 else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, h, aov, cnt.shades);
                 else done = path_hit<F>(S, P, st, h, aov, cnt.shades);
                 alive = true;
                 if (done) {
-                    finish(st, pixel, sample, aov);
-                    const int g = s >> 6;
-                    if (++sample < C.g_cs1[g]) {
+                    // trace_sample's epilogue (src/trace.jl:625-648) on the slot's running means
+                    cnt.paths++;
+                    v3 radiance = st.radiance;
+                    if (!all_finite(radiance)) radiance = V3(0, 0, 0);
+                    const float mr = max3(radiance);
+                    if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
+                    const float w = acc.w;
+                    const float omw = 1 - w;
+                    const bool hit = st.flags & F_HIT;
+                    const bool env = !hit && !P.envhidden && S.nenvs != 0;
+                    const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
+                    if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
+                    acc.im.x = acc.im.x * omw + target.x * w;
+                    acc.im.y = acc.im.y * omw + target.y * w;
+                    acc.im.z = acc.im.z * omw + target.z * w;
+                    acc.im.w = acc.im.w * omw + target.w * w;
+                    if (hit || env) acc.hits += 1;
+                    if (++sample < C.g_cs1[s >> 6]) {
+                        acc.w = 1.0f / (float)(sample - P.first + 1);
                         start_path(P, pixel % P.width, pixel / P.width, pixel, sample, st);
-                    } else {
+                    } else {  // the slot's chunk is done: its pixel's running means back to HBM
                         alive = false;
+                        A.image[pixel] = acc.im;
+                        A.albedo[pixel] = make_float4(acc.al.x, acc.al.y, acc.al.z, 0.0f);
+                        A.normal[pixel] = make_float4(acc.nr.x, acc.nr.y, acc.nr.z, 0.0f);
+                        A.hits[pixel] += acc.hits;
                     }
                 }
                 if (alive) {
-                    wf_store<F>(recs + (size_t)s * RQ, st, pixel, sample);
+                    wf_store<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
                     issue(s, st);
+                    pend = s;
                 }
             }
-            wf_push(C, ring[WF_TRAV], NP, WF_TRAV, alive, s);
-            // slots whose chunk is done: the last one of a group publishes the tile's running means
+            // slots whose chunk is done: the last one of its group publishes the tile
             const bool fin = mine && !alive;
             if (__builtin_amdgcn_ballot_w64(fin)) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 bool last = false;
-                int g = 0;
-                if (fin) {
-                    g = s >> 6;
-                    last = __hip_atomic_fetch_add(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 1;
-                }
+                const int g = s >> 6;
+                if (fin) last = __hip_atomic_fetch_add(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 1;
                 if (__builtin_amdgcn_ballot_w64(last)) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                     if (last) {
                         if (C.g_uc[g] + 1 < nchunks)
                             __hip_atomic_store(A.tile_done + C.g_tile[g], C.g_uc[g] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (!lds_ld(&C.exhausted))
+                            __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_sub(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
             }
@@ -1606,28 +1631,26 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
         }
 
         // ---------------------------------------------------------------- traverse
-        // refill: lanes without a query take the oldest waiting ones (first pop at once)
-        if (busy < 64 && tl > 0) {
-            const unsigned long long idle_m = ~busy_m;
-            unsigned base;
-            const int n = wf_claim(C, WF_TRAV, 64 - busy, base);
-            if (n > 0) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                const int r = lane_rank(idle_m);
-                if (qslot < 0 && r < n) {
-                    const int s = wf_take(C, ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    const float4 o = q_o[s], d = q_d[s];
-                    const unsigned root = __float_as_uint(o.w);
-                    qslot = s | ((root >> 30) == T_INST ? 1 << 16 : 0);
-                    query_begin(T, V3(o.x, o.y, o.z), V3(d.x, d.y, d.z), root, stack);
+        unsigned tq = tl;
+        for (int it = 0; it < JT_WF_TRAV_ITERS; it++) {
+            // refill: lanes without a query take the oldest waiting ones (their first pop at once)
+            if (tq > 0 && (64 - busy >= P.wf_refill || busy == 0)) {
+                unsigned base;
+                const int n = wf_claim(C, WF_TRAV, 64 - busy, base);
+                if (n > 0) {
+                    const int r = lane_rank(__builtin_amdgcn_ballot_w64(qslot < 0));
+                    if (qslot < 0 && r < n) {
+                        const int s = wf_take(C, ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
+                        const float4 o = q_o[s], d = q_d[s];
+                        const unsigned root = __float_as_uint(o.w);
+                        qslot = s | ((root >> 30) == T_INST ? 1 << 16 : 0);
+                        query_begin(T, V3(o.x, o.y, o.z), V3(d.x, d.y, d.z), root, stack);
 #pragma unroll
-                    for (int k = 0; k < JT_FIRST_POP; k++)
-                        if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
+                        for (int k = 0; k < JT_FIRST_POP; k++)
+                            if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
+                    }
                 }
             }
-        }
-        {
             const bool wantp = T.nprim > 0;
             const bool wantn = T.nprim == 0 && T.sp > 0;
             const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
@@ -1639,19 +1662,27 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                 for (int k = 0; k < JT_NODE_REPEAT; k++)
                     if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
             }
-        }
-        // finished queries: the result to LDS, the slot onto its shading ring
-        const bool fin = qslot >= 0 && (T.sp | T.nprim) == 0;
-        if (__builtin_amdgcn_ballot_w64(fin)) {
-            const int s = qslot & 0xffff;
-            const bool light = (qslot >> 16) != 0;
-            if (fin) {
-                r_h[s] = make_float4(__int_as_float(T.h_inst), __int_as_float(T.h_elem), T.h_u, T.h_v);
-                r_t[s] = T.tmax;
+            // finished queries: the result to LDS, the slot onto its shading ring
+            const bool fin = qslot >= 0 && (T.sp | T.nprim) == 0;
+            if (__builtin_amdgcn_ballot_w64(fin)) {
+                const int s = qslot & 0xffff;
+                const bool light = (qslot >> 16) != 0;
+                if (fin) {
+                    r_h[s] = make_float4(__int_as_float(T.h_inst), __int_as_float(T.h_elem), T.h_u, T.h_v);
+                    r_t[s] = T.tmax;
+                }
+                lds_order();
+                wf_push(C, ring[WF_SCENE], NP, WF_SCENE, fin && !light, s);
+                wf_push(C, ring[WF_LIGHT], NP, WF_LIGHT, fin && light, s);
+                if (fin) qslot = -1;
             }
-            wf_push(C, ring[WF_SCENE], NP, WF_SCENE, fin && !light, s);
-            wf_push(C, ring[WF_LIGHT], NP, WF_LIGHT, fin && light, s);
-            if (fin) qslot = -1;
+            busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
+            // back to the job choice when this wave runs dry or a full shading batch waits
+            const unsigned c2 = lane < 6 ? lds_ld(reinterpret_cast<const unsigned*>(&C) + lane) : 0u;
+            tq = __builtin_amdgcn_readlane(c2, 3) - __builtin_amdgcn_readlane(c2, 0);
+            const unsigned s2 = __builtin_amdgcn_readlane(c2, 4) - __builtin_amdgcn_readlane(c2, 1);
+            const unsigned l2 = __builtin_amdgcn_readlane(c2, 5) - __builtin_amdgcn_readlane(c2, 2);
+            if ((busy == 0 && tq == 0) || (s2 > l2 ? s2 : l2) >= (unsigned)P.wait_lanes) break;
         }
     }
     unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
@@ -2528,6 +2559,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             if (const char* g = std::getenv("JT_WF_GROUPS")) P.wf_groups = std::max(1, std::min(WF_GMAX, std::atoi(g)));
             P.wait_lanes = 56;
             if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
+            P.wf_refill = 8;
+            if (const char* r = std::getenv("JT_WF_REFILL")) P.wf_refill = std::max(1, std::min(64, std::atoi(r)));
         }
     }
 

@@ -8,9 +8,10 @@ scripts/gpu_step.sh 300 $O/pytest_wf.log timeout -k 10 280 python -u -m pytest t
 grep -q " passed" $O/pytest_wf.log || exit 1
 grep -q "failed" $O/pytest_wf.log && exit 1
 scripts/gpu_step.sh 120 $O/bench_mk.log timeout -k 10 100 python bench.py --no-cpu-baseline --steps 2 || exit 1
-for g in 5 6; do for wl in 40 56 64; do
-  JT_WF=1 JT_WF_GROUPS=$g JT_WAIT_LANES=$wl scripts/gpu_step.sh 120 $O/bench_wf_g${g}_w${wl}.log timeout -k 10 100 python bench.py --no-cpu-baseline --steps 2 || exit 1
-done; done
+for cfg in "5 56 8" "4 56 8" "5 64 8" "5 48 8" "5 56 2" "5 56 24" "3 56 8"; do
+  set -- $cfg
+  JT_WF=1 JT_WF_GROUPS=$1 JT_WAIT_LANES=$2 JT_WF_REFILL=$3 scripts/gpu_step.sh 120 $O/bench_wf_g$1_w$2_r$3.log timeout -k 10 100 python bench.py --no-cpu-baseline --steps 2 || exit 1
+done
 grep -h '"value"' $O/bench_*.log | python -c "
 import sys, json
 for l in sys.stdin:
