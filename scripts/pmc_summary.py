@@ -17,6 +17,8 @@ def match(name):
     if "trace_kernel" not in name:
         return False
     targs = name[name.index("<") + 1:name.index(">")].split(",")
+    if "trace_kernel_wf" in name:  # <SAMPLER, COUNT, F, LDSM>
+        return targs[1].strip() == "0"
     return len(targs) >= 4 and targs[3].strip() == "0"  # COUNT=0: the timed kernel, not the counting pass
 agg = collections.defaultdict(list)
 meta = {}
