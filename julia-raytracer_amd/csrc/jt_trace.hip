@@ -1405,6 +1405,16 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     int qslot = -1;  // the slot whose query this lane runs (-1: none); bit 16: a light query
     int pend = -1;   // a slot this lane shaded whose next query waits to be pushed (after its record store)
     unsigned idle_iters = 0;
+#if JT_STAMPS
+    // diagnostic build: cycles per job kind, traversal lane counts, batch sizes (scripts/stamps.py wf)
+    unsigned long long sw[15] = {0};
+    unsigned long long tj = __builtin_amdgcn_s_memtime();
+#define WF_STAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sw[k] += t_ - tj; tj = t_; } while (0)
+#define WF_ADD(k, v) (sw[k] += (v))
+#else
+#define WF_STAMP(k) ((void)0)
+#define WF_ADD(k, v) ((void)0)
+#endif
 
     // a slot's pending query (LDS): origin, direction, root
     auto issue = [&](int s, const Path& st) {
@@ -1463,6 +1473,8 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
         }
         const unsigned qmax = sl > ll ? sl : ll;
         int job;  // 0 traverse, 1 start group, 2 shade scene ring, 3 shade light ring, 5 nothing to do
+        WF_STAMP(14);
+        WF_ADD(13, 1);
         if (gsel >= 0) job = 1;
         else if (qmax >= (unsigned)P.wait_lanes || (qmax > 0 && tl == 0 && (unsigned)busy < qmax)) job = sl >= ll ? 2 : 3;
         else if (busy > 0 || tl > 0) job = 0;
@@ -1478,6 +1490,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                 if (lane == 0) atomicAdd(A.counters + 7, 1ull);
                 break;
             }
+            WF_STAMP(3);
             continue;
         }
         idle_iters = 0;
@@ -1546,6 +1559,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             }
             const int started = lane_count(__builtin_amdgcn_ballot_w64(in_image));
             if (lane == 0) __hip_atomic_store(&C.g_left[g], started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            WF_STAMP(2);
             continue;
         }
 
@@ -1555,6 +1569,9 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             unsigned base;
             const int n = wf_claim(C, q, 64, base);
             if (n == 0) continue;
+            WF_ADD(7, 1);
+            WF_ADD(8, n);
+            WF_ADD(11, q == WF_LIGHT ? 1 : 0);
             const bool mine = lane < n;
             int s = -1;
             bool alive = false;
@@ -1627,16 +1644,20 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                     }
                 }
             }
+            WF_STAMP(1);
             continue;
         }
 
         // ---------------------------------------------------------------- traverse
         unsigned tq = tl;
+        WF_ADD(12, tq);
         for (int it = 0; it < JT_WF_TRAV_ITERS; it++) {
             // refill: lanes without a query take the oldest waiting ones (their first pop at once)
             if (tq > 0 && (64 - busy >= P.wf_refill || busy == 0)) {
                 unsigned base;
                 const int n = wf_claim(C, WF_TRAV, 64 - busy, base);
+                WF_ADD(9, 1);
+                WF_ADD(10, n);
                 if (n > 0) {
                     const int r = lane_rank(__builtin_amdgcn_ballot_w64(qslot < 0));
                     if (qslot < 0 && r < n) {
@@ -1655,6 +1676,9 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             const bool wantn = T.nprim == 0 && T.sp > 0;
             const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
             const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
+            WF_ADD(4, 1);
+            WF_ADD(5, np >= nn ? np : nn);
+            WF_ADD(6, np + nn);
             if (np >= nn) {
                 if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
             } else {
@@ -1684,7 +1708,14 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             const unsigned l2 = __builtin_amdgcn_readlane(c2, 5) - __builtin_amdgcn_readlane(c2, 2);
             if ((busy == 0 && tq == 0) || (s2 > l2 ? s2 : l2) >= (unsigned)P.wait_lanes) break;
         }
+        WF_STAMP(0);
     }
+#if JT_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < 15; k++) atomicAdd(A.counters + 8 + k, sw[k]);
+#endif
+#undef WF_STAMP
+#undef WF_ADD
     unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
                      COUNT ? cnt.shades : 0u};
 #pragma unroll
