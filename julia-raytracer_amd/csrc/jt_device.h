@@ -157,6 +157,7 @@ struct DParams {
     int chunk;  // samples per work unit (a tile's chunks run in order)
     int wf_groups;  // WF body: 64-slot path groups per workgroup
     int wf_refill;  // WF body: idle lanes that make a traversal step first take new queries
+    int wf_shaders; // WF body: shading waves per workgroup (the others traverse)
     unsigned long long seed;
 };
 

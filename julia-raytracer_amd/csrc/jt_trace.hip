@@ -1402,7 +1402,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     Trav T;
     T.sp = 0;
     T.nprim = 0;
-    int qslot = -1;  // the slot whose query this lane runs (-1: none); bit 16: a light query
+    int qslot = -1;  // the slot whose query this lane runs (-1: none)
     int pend = -1;   // a slot this lane shaded whose next query waits to be pushed (after its record store)
     unsigned idle_iters = 0;
 #if JT_STAMPS
@@ -1428,155 +1428,219 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
         else cnt.rays++;
     };
 
-    for (;;) {
-        // queries issued by the last shading job: their records are stored, now publish them
-        if (__builtin_amdgcn_ballot_w64(pend >= 0)) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            wf_push(C, ring[WF_TRAV], NP, WF_TRAV, pend >= 0, pend);
-            pend = -1;
-        }
-        if (lds_ld(&C.abort)) {
-            if (lane == 0) atomicAdd(A.counters + 7, 1ull);
-            break;
-        }
-        // ---------------------------------------------------------------- pick the wave's job
-        // the control words, one per lane (one LDS round trip)
+    // Roles: the last P.wf_shaders waves of the workgroup shade (and start slot groups); the others
+    // only traverse. A shading wave never holds a suspended query, so it runs each path's
+    // sample_lights_pdf instance queries (short: one light's BLAS) inline on its own lanes' stacks
+    // right after path_hit, with the path in registers: only closest-hit scene queries go through
+    // the rings. Traversal waves refill their lanes from the ring and keep stepping.
+    const bool shader = (int)(threadIdx.x >> 6) >= BLOCK / 64 - P.wf_shaders;
+    auto ctl = [&]() {  // one LDS round trip: the control words, one per lane, read by all
         const unsigned cv = lane < 8 ? lds_ld(reinterpret_cast<const unsigned*>(&C) + lane) : 0u;
-        const unsigned tl = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
-        const unsigned sl = __builtin_amdgcn_readlane(cv, 4) - __builtin_amdgcn_readlane(cv, 1);
-        const unsigned ll = __builtin_amdgcn_readlane(cv, 5) - __builtin_amdgcn_readlane(cv, 2);
-        const unsigned attn = __builtin_amdgcn_readlane(cv, 6);
-        int busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
-        int gsel = -1;
-        if (attn) {  // a group to start: an idle one while units remain, or one whose tile is ready
-            if (lane == 0) {
-                for (int g = 0; g < G && gsel < 0; g++) {
-                    if (!((attn >> g) & 1)) continue;
-                    const int gl = lds_ld(&C.g_left[g]);
-                    int expect = gl;
-                    if (gl == -2) {
-                        if (__hip_atomic_load(A.tile_done + C.g_tile[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= C.g_uc[g] &&
-                            __hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
-                            gsel = g;
-                    } else if (gl == -1) {
-                        if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -4, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                            gsel = g;
-                            __hip_atomic_fetch_add(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                    }
-                    if (gsel >= 0) __hip_atomic_fetch_and(&C.attn, ~(1u << g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return cv;
+    };
+    auto finished_all = [&]() { return lds_ld(&C.exhausted) && lds_ld(&C.live) == 0u; };
+
+    if (!shader) {
+        // ================================================================ traversal wave
+        for (;;) {
+            if (lds_ld(&C.abort)) break;
+            unsigned cv = ctl();
+            unsigned tq = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
+            int busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
+            if (busy == 0 && tq == 0) {
+                if (finished_all()) break;
+                __builtin_amdgcn_s_sleep(2);
+                if (++idle_iters > (1u << 27)) {  // bounded: never expected
+                    if (lane == 0) atomicAdd(A.counters + 7, 1ull);
+                    break;
                 }
+                WF_STAMP(3);
+                continue;
             }
-            gsel = __builtin_amdgcn_readfirstlane(gsel);
-        }
-        const unsigned qmax = sl > ll ? sl : ll;
-        int job;  // 0 traverse, 1 start group, 2 shade scene ring, 3 shade light ring, 5 nothing to do
-        WF_STAMP(14);
-        WF_ADD(13, 1);
-        if (gsel >= 0) job = 1;
-        else if (qmax >= (unsigned)P.wait_lanes || (qmax > 0 && tl == 0 && (unsigned)busy < qmax)) job = sl >= ll ? 2 : 3;
-        else if (busy > 0 || tl > 0) job = 0;
-        else if (qmax > 0) job = sl >= ll ? 2 : 3;
-        else job = 5;
-
-        if (job == 5) {
-            // nothing here: the workgroup is done, or other waves hold its last queries / a tile wait
-            const bool done = lds_ld(&C.exhausted) && lds_ld(&C.live) == 0u;
-            if (done) break;
-            __builtin_amdgcn_s_sleep(4);
-            if (++idle_iters > (1u << 26)) {  // bounded: never expected
-                if (lane == 0) atomicAdd(A.counters + 7, 1ull);
-                break;
-            }
-            WF_STAMP(3);
-            continue;
-        }
-        idle_iters = 0;
-
-        if (job == 1) {
-            // ------------------------------------------------------------ start a slot group
-            const int g = gsel;
-            int state = 0;
-            if (lane == 0) {
-                state = C.g_left[g];
-                if (state == -4) {  // idle group: fetch a unit (this XCD's band first, then the others)
-                    int unit_uc = -1, unit_t = 0;
-                    for (;;) {
-                        const int bk = lds_ld(&C.band_k);
-                        if (bk >= NBANDS) break;
-                        const int band = (int)((xcc + (unsigned)bk) & (NBANDS - 1));
-                        const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
-                        const unsigned unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
-                        if (unit < (unsigned)bn * (unsigned)nchunks) {
-                            unit_uc = (int)(unit / (unsigned)bn);
-                            unit_t = bt0 + (int)(unit % (unsigned)bn);
-                            break;
-                        }
-                        int expect = bk;
-                        __hip_atomic_compare_exchange_strong(&C.band_k, &expect, bk + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                    if (unit_uc < 0) {  // no units left: this group stays idle
-                        __hip_atomic_store(&C.exhausted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_sub(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        state = -1;
-                    } else {
-                        C.g_tile[g] = unit_t;
-                        C.g_uc[g] = unit_uc;
-                        const int cs0 = s_begin + unit_uc * P.chunk;
-                        C.g_cs1[g] = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
-                        if (unit_uc > 0 &&
-                            __hip_atomic_load(A.tile_done + unit_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unit_uc) {
-                            // its tile's previous chunk is not published yet: start it later
-                            __hip_atomic_store(&C.g_left[g], -2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            state = -2;
+            idle_iters = 0;
+            WF_ADD(12, tq);
+            for (int it = 0; it < JT_WF_TRAV_ITERS; it++) {
+                // refill: lanes without a query take the oldest waiting ones (their first pop at once)
+                if (tq > 0 && (64 - busy >= P.wf_refill || busy == 0)) {
+                    unsigned base;
+                    const int n = wf_claim(C, WF_TRAV, 64 - busy, base);
+                    WF_ADD(9, 1);
+                    WF_ADD(10, n);
+                    if (n > 0) {
+                        const int r = lane_rank(__builtin_amdgcn_ballot_w64(qslot < 0));
+                        if (qslot < 0 && r < n) {
+                            const int s = wf_take(C, ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
+                            const float4 o = q_o[s], d = q_d[s];
+                            qslot = s;
+                            query_begin(T, V3(o.x, o.y, o.z), V3(d.x, d.y, d.z), __float_as_uint(o.w), stack);
+#pragma unroll
+                            for (int k = 0; k < JT_FIRST_POP; k++)
+                                if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
                         }
                     }
                 }
+                const bool wantp = T.nprim > 0;
+                const bool wantn = T.nprim == 0 && T.sp > 0;
+                const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
+                const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
+                WF_ADD(4, 1);
+                WF_ADD(5, np >= nn ? np : nn);
+                WF_ADD(6, np + nn);
+                if (np >= nn) {
+                    if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < JT_NODE_REPEAT; k++)
+                        if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
+                }
+                // finished queries: the result to LDS, the slot onto the shading ring
+                const bool fin = qslot >= 0 && (T.sp | T.nprim) == 0;
+                if (__builtin_amdgcn_ballot_w64(fin)) {
+                    if (fin) {
+                        r_h[qslot] = make_float4(__int_as_float(T.h_inst), __int_as_float(T.h_elem), T.h_u, T.h_v);
+                        r_t[qslot] = T.tmax;
+                    }
+                    lds_order();
+                    wf_push(C, ring[WF_SCENE], NP, WF_SCENE, fin, qslot);
+                    if (fin) qslot = -1;
+                }
+                busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
+                cv = ctl();
+                tq = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
+                if (busy == 0 && tq == 0) break;
             }
-            state = __builtin_amdgcn_readfirstlane(state);
-            if (state == -1 || state == -2) continue;
-            lds_order();
-            const int ut = C.g_tile[g], uc = C.g_uc[g];
-            if (uc > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's running means
-            const int i = (ut % tiles_x) * 8 + (lane & 7), j = (ut / tiles_x) * 8 + (lane >> 3);
-            const bool in_image = i < P.width && j < P.height;
-            const int s = g * 64 + lane;
-            const int cs0 = s_begin + uc * P.chunk;
-            const int pixel = j * P.width + i;
-            if (in_image) {
-                const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
-                WfAcc acc{im, V3(al.x, al.y, al.z), V3(nr.x, nr.y, nr.z), 0, 1.0f / (float)(cs0 - P.first + 1)};
-                Path st;
-                start_path(P, i, j, pixel, cs0, st);
-                wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0, acc);
-                issue(s, st);
-                pend = s;
-            }
-            const int started = lane_count(__builtin_amdgcn_ballot_w64(in_image));
-            if (lane == 0) __hip_atomic_store(&C.g_left[g], started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            WF_STAMP(2);
-            continue;
+            WF_STAMP(0);
         }
-
-        if (job >= 2) {
+    } else {
+        // ================================================================ shading wave
+        for (;;) {
+            // queries issued by the last job: their records are stored, now publish them
+            if (__builtin_amdgcn_ballot_w64(pend >= 0)) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                wf_push(C, ring[WF_TRAV], NP, WF_TRAV, pend >= 0, pend);
+                pend = -1;
+            }
+            if (lds_ld(&C.abort)) break;
+            const unsigned cv = ctl();
+            const unsigned tl = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
+            const unsigned sl = __builtin_amdgcn_readlane(cv, 4) - __builtin_amdgcn_readlane(cv, 1);
+            const unsigned attn = __builtin_amdgcn_readlane(cv, 6);
+            int gsel = -1;
+            if (attn) {  // a group to start: an idle one while units remain, or one whose tile is ready
+                if (lane == 0) {
+                    for (int g = 0; g < G && gsel < 0; g++) {
+                        if (!((attn >> g) & 1)) continue;
+                        const int gl = lds_ld(&C.g_left[g]);
+                        int expect = gl;
+                        if (gl == -2) {
+                            if (__hip_atomic_load(A.tile_done + C.g_tile[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= C.g_uc[g] &&
+                                __hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
+                                gsel = g;
+                        } else if (gl == -1) {
+                            if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -4, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                                gsel = g;
+                                __hip_atomic_fetch_add(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                        }
+                        if (gsel >= 0) __hip_atomic_fetch_and(&C.attn, ~(1u << g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                gsel = __builtin_amdgcn_readfirstlane(gsel);
+            }
+            WF_STAMP(14);
+            WF_ADD(13, 1);
+            if (gsel >= 0) {
+                // ------------------------------------------------------------ start a slot group
+                const int g = gsel;
+                int state = 0;
+                if (lane == 0) {
+                    state = C.g_left[g];
+                    if (state == -4) {  // idle group: fetch a unit (this XCD's band first, then the others)
+                        int unit_uc = -1, unit_t = 0;
+                        for (;;) {
+                            const int bk = lds_ld(&C.band_k);
+                            if (bk >= NBANDS) break;
+                            const int band = (int)((xcc + (unsigned)bk) & (NBANDS - 1));
+                            const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
+                            const unsigned unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
+                            if (unit < (unsigned)bn * (unsigned)nchunks) {
+                                unit_uc = (int)(unit / (unsigned)bn);
+                                unit_t = bt0 + (int)(unit % (unsigned)bn);
+                                break;
+                            }
+                            int expect = bk;
+                            __hip_atomic_compare_exchange_strong(&C.band_k, &expect, bk + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        if (unit_uc < 0) {  // no units left: this group stays idle
+                            __hip_atomic_store(&C.exhausted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_sub(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            state = -1;
+                        } else {
+                            C.g_tile[g] = unit_t;
+                            C.g_uc[g] = unit_uc;
+                            const int cs0 = s_begin + unit_uc * P.chunk;
+                            C.g_cs1[g] = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
+                            if (unit_uc > 0 &&
+                                __hip_atomic_load(A.tile_done + unit_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unit_uc) {
+                                // its tile's previous chunk is not published yet: start it later
+                                __hip_atomic_store(&C.g_left[g], -2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                state = -2;
+                            }
+                        }
+                    }
+                }
+                state = __builtin_amdgcn_readfirstlane(state);
+                if (state == -1 || state == -2) continue;
+                lds_order();
+                const int ut = C.g_tile[g], uc = C.g_uc[g];
+                if (uc > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's running means
+                const int i = (ut % tiles_x) * 8 + (lane & 7), j = (ut / tiles_x) * 8 + (lane >> 3);
+                const bool in_image = i < P.width && j < P.height;
+                const int s = g * 64 + lane;
+                const int cs0 = s_begin + uc * P.chunk;
+                const int pixel = j * P.width + i;
+                if (in_image) {
+                    const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
+                    WfAcc acc{im, V3(al.x, al.y, al.z), V3(nr.x, nr.y, nr.z), 0, 1.0f / (float)(cs0 - P.first + 1)};
+                    Path st;
+                    start_path(P, i, j, pixel, cs0, st);
+                    wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0, acc);
+                    issue(s, st);
+                    pend = s;
+                }
+                const int started = lane_count(__builtin_amdgcn_ballot_w64(in_image));
+                if (lane == 0) __hip_atomic_store(&C.g_left[g], started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                WF_STAMP(2);
+                continue;
+            }
+            // shade when a full batch waits, or when the traversal waves are about to run dry
+            if (!(sl >= (unsigned)P.wait_lanes || (sl > 0 && tl < (unsigned)P.wf_refill * 4))) {
+                if (sl == 0 && tl == 0 && finished_all()) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++idle_iters > (1u << 27)) {  // bounded: never expected
+                    if (lane == 0) atomicAdd(A.counters + 7, 1ull);
+                    break;
+                }
+                WF_STAMP(3);
+                continue;
+            }
+            idle_iters = 0;
             // ------------------------------------------------------------ shade a batch
-            const int q = job == 2 ? WF_SCENE : WF_LIGHT;
             unsigned base;
-            const int n = wf_claim(C, q, 64, base);
+            const int n = wf_claim(C, WF_SCENE, 64, base);
             if (n == 0) continue;
             WF_ADD(7, 1);
             WF_ADD(8, n);
-            WF_ADD(11, q == WF_LIGHT ? 1 : 0);
             const bool mine = lane < n;
             int s = -1;
             bool alive = false;
             if (mine) {
-                s = wf_take(C, ring[q], (base + (unsigned)lane) % (unsigned)NP);
+                s = wf_take(C, ring[WF_SCENE], (base + (unsigned)lane) % (unsigned)NP);
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 Path st;
                 WfAcc acc;
@@ -1586,9 +1650,18 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                 const Hit h{__float_as_int(hh.x), __float_as_int(hh.y), hh.z, hh.w, r_t[s], __float_as_int(hh.x) >= 0};
                 const WfAov aov{&acc};
                 bool done;
-                if (SAMPLER == 1 && q == WF_LIGHT) done = light_hit<F>(S, P, st, h);
-                else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, h, aov, cnt.shades);
+                if (SAMPLER == 2) done = naive_hit<F>(S, P, st, h, aov, cnt.shades);
                 else done = path_hit<F>(S, P, st, h, aov, cnt.shades);
+                // sample_lights_pdf's instance queries, inline (src/trace.jl:1018-1044)
+                while (SAMPLER == 1 && !done && st.phase == PH_LIGHT) {
+                    cnt.light_queries++;
+                    query_begin(T, st.lq, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
+                    while (T.sp > 0 || T.nprim > 0) {
+                        if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+                        else node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
+                    }
+                    done = light_hit<F>(S, P, st, query_hit(T));
+                }
                 alive = true;
                 if (done) {
                     // trace_sample's epilogue (src/trace.jl:625-648) on the slot's running means
@@ -1645,70 +1718,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                 }
             }
             WF_STAMP(1);
-            continue;
         }
-
-        // ---------------------------------------------------------------- traverse
-        unsigned tq = tl;
-        WF_ADD(12, tq);
-        for (int it = 0; it < JT_WF_TRAV_ITERS; it++) {
-            // refill: lanes without a query take the oldest waiting ones (their first pop at once)
-            if (tq > 0 && (64 - busy >= P.wf_refill || busy == 0)) {
-                unsigned base;
-                const int n = wf_claim(C, WF_TRAV, 64 - busy, base);
-                WF_ADD(9, 1);
-                WF_ADD(10, n);
-                if (n > 0) {
-                    const int r = lane_rank(__builtin_amdgcn_ballot_w64(qslot < 0));
-                    if (qslot < 0 && r < n) {
-                        const int s = wf_take(C, ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
-                        const float4 o = q_o[s], d = q_d[s];
-                        const unsigned root = __float_as_uint(o.w);
-                        qslot = s | ((root >> 30) == T_INST ? 1 << 16 : 0);
-                        query_begin(T, V3(o.x, o.y, o.z), V3(d.x, d.y, d.z), root, stack);
-#pragma unroll
-                        for (int k = 0; k < JT_FIRST_POP; k++)
-                            if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
-                    }
-                }
-            }
-            const bool wantp = T.nprim > 0;
-            const bool wantn = T.nprim == 0 && T.sp > 0;
-            const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
-            const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
-            WF_ADD(4, 1);
-            WF_ADD(5, np >= nn ? np : nn);
-            WF_ADD(6, np + nn);
-            if (np >= nn) {
-                if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-            } else {
-#pragma unroll
-                for (int k = 0; k < JT_NODE_REPEAT; k++)
-                    if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
-            }
-            // finished queries: the result to LDS, the slot onto its shading ring
-            const bool fin = qslot >= 0 && (T.sp | T.nprim) == 0;
-            if (__builtin_amdgcn_ballot_w64(fin)) {
-                const int s = qslot & 0xffff;
-                const bool light = (qslot >> 16) != 0;
-                if (fin) {
-                    r_h[s] = make_float4(__int_as_float(T.h_inst), __int_as_float(T.h_elem), T.h_u, T.h_v);
-                    r_t[s] = T.tmax;
-                }
-                lds_order();
-                wf_push(C, ring[WF_SCENE], NP, WF_SCENE, fin && !light, s);
-                wf_push(C, ring[WF_LIGHT], NP, WF_LIGHT, fin && light, s);
-                if (fin) qslot = -1;
-            }
-            busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
-            // back to the job choice when this wave runs dry or a full shading batch waits
-            const unsigned c2 = lane < 6 ? lds_ld(reinterpret_cast<const unsigned*>(&C) + lane) : 0u;
-            tq = __builtin_amdgcn_readlane(c2, 3) - __builtin_amdgcn_readlane(c2, 0);
-            const unsigned s2 = __builtin_amdgcn_readlane(c2, 4) - __builtin_amdgcn_readlane(c2, 1);
-            const unsigned l2 = __builtin_amdgcn_readlane(c2, 5) - __builtin_amdgcn_readlane(c2, 2);
-            if ((busy == 0 && tq == 0) || (s2 > l2 ? s2 : l2) >= (unsigned)P.wait_lanes) break;
-        }
-        WF_STAMP(0);
     }
 #if JT_STAMPS
     if (lane == 0)
@@ -2592,6 +2602,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
             P.wf_refill = 8;
             if (const char* r = std::getenv("JT_WF_REFILL")) P.wf_refill = std::max(1, std::min(64, std::atoi(r)));
+            P.wf_shaders = 1;
+            if (const char* r = std::getenv("JT_WF_SHADERS")) P.wf_shaders = std::max(1, std::min(3, std::atoi(r)));
         }
     }
 
