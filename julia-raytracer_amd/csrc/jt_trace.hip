@@ -1428,11 +1428,12 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
         else cnt.rays++;
     };
 
-    // Roles: the last P.wf_shaders waves of the workgroup shade (and start slot groups); the others
-    // only traverse. A shading wave never holds a suspended query, so it runs each path's
-    // sample_lights_pdf instance queries (short: one light's BLAS) inline on its own lanes' stacks
-    // right after path_hit, with the path in registers: only closest-hit scene queries go through
-    // the rings. Traversal waves refill their lanes from the ring and keep stepping.
+    // Roles: the last P.wf_shaders waves of the workgroup only shade and start slot groups; the
+    // others traverse, refilling their lanes from the ring, and shade too whenever they hold no
+    // query and none waits (work-conserving). A wave shades only with no query in flight, so it
+    // runs each path's sample_lights_pdf instance queries (short: one light's BLAS) inline on its
+    // own lanes' stacks right after path_hit, with the path in registers: only closest-hit scene
+    // queries go through the rings.
     const bool shader = (int)(threadIdx.x >> 6) >= BLOCK / 64 - P.wf_shaders;
     auto ctl = [&]() {  // one LDS round trip: the control words, one per lane, read by all
         const unsigned cv = lane < 8 ? lds_ld(reinterpret_cast<const unsigned*>(&C) + lane) : 0u;
@@ -1440,23 +1441,22 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     };
     auto finished_all = [&]() { return lds_ld(&C.exhausted) && lds_ld(&C.live) == 0u; };
 
-    if (!shader) {
-        // ================================================================ traversal wave
-        for (;;) {
-            if (lds_ld(&C.abort)) break;
-            unsigned cv = ctl();
-            unsigned tq = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
-            int busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
-            if (busy == 0 && tq == 0) {
-                if (finished_all()) break;
-                __builtin_amdgcn_s_sleep(2);
-                if (++idle_iters > (1u << 27)) {  // bounded: never expected
-                    if (lane == 0) atomicAdd(A.counters + 7, 1ull);
-                    break;
-                }
-                WF_STAMP(3);
-                continue;
-            }
+    for (;;) {
+        // queries issued by the last shading job: their records are stored, now publish them
+        if (__builtin_amdgcn_ballot_w64(pend >= 0)) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            wf_push(C, ring[WF_TRAV], NP, WF_TRAV, pend >= 0, pend);
+            pend = -1;
+        }
+        if (lds_ld(&C.abort)) break;
+        unsigned cv = ctl();
+        unsigned tq = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
+        const unsigned tl = tq;
+        const unsigned sl = __builtin_amdgcn_readlane(cv, 4) - __builtin_amdgcn_readlane(cv, 1);
+        const unsigned attn = __builtin_amdgcn_readlane(cv, 6);
+        int busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
+        if (!shader && (busy > 0 || tq > 0)) {
+            // ------------------------------------------------------------ traverse
             idle_iters = 0;
             WF_ADD(12, tq);
             for (int it = 0; it < JT_WF_TRAV_ITERS; it++) {
@@ -1510,215 +1510,203 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                 if (busy == 0 && tq == 0) break;
             }
             WF_STAMP(0);
+            continue;
         }
-    } else {
-        // ================================================================ shading wave
-        for (;;) {
-            // queries issued by the last job: their records are stored, now publish them
-            if (__builtin_amdgcn_ballot_w64(pend >= 0)) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                wf_push(C, ring[WF_TRAV], NP, WF_TRAV, pend >= 0, pend);
-                pend = -1;
-            }
-            if (lds_ld(&C.abort)) break;
-            const unsigned cv = ctl();
-            const unsigned tl = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
-            const unsigned sl = __builtin_amdgcn_readlane(cv, 4) - __builtin_amdgcn_readlane(cv, 1);
-            const unsigned attn = __builtin_amdgcn_readlane(cv, 6);
-            int gsel = -1;
-            if (attn) {  // a group to start: an idle one while units remain, or one whose tile is ready
-                if (lane == 0) {
-                    for (int g = 0; g < G && gsel < 0; g++) {
-                        if (!((attn >> g) & 1)) continue;
-                        const int gl = lds_ld(&C.g_left[g]);
-                        int expect = gl;
-                        if (gl == -2) {
-                            if (__hip_atomic_load(A.tile_done + C.g_tile[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= C.g_uc[g] &&
-                                __hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
-                                gsel = g;
-                        } else if (gl == -1) {
-                            if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -4, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                                gsel = g;
-                                __hip_atomic_fetch_add(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            }
-                        }
-                        if (gsel >= 0) __hip_atomic_fetch_and(&C.attn, ~(1u << g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-                gsel = __builtin_amdgcn_readfirstlane(gsel);
-            }
-            WF_STAMP(14);
-            WF_ADD(13, 1);
-            if (gsel >= 0) {
-                // ------------------------------------------------------------ start a slot group
-                const int g = gsel;
-                int state = 0;
-                if (lane == 0) {
-                    state = C.g_left[g];
-                    if (state == -4) {  // idle group: fetch a unit (this XCD's band first, then the others)
-                        int unit_uc = -1, unit_t = 0;
-                        for (;;) {
-                            const int bk = lds_ld(&C.band_k);
-                            if (bk >= NBANDS) break;
-                            const int band = (int)((xcc + (unsigned)bk) & (NBANDS - 1));
-                            const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
-                            const unsigned unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
-                            if (unit < (unsigned)bn * (unsigned)nchunks) {
-                                unit_uc = (int)(unit / (unsigned)bn);
-                                unit_t = bt0 + (int)(unit % (unsigned)bn);
-                                break;
-                            }
-                            int expect = bk;
-                            __hip_atomic_compare_exchange_strong(&C.band_k, &expect, bk + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                        if (unit_uc < 0) {  // no units left: this group stays idle
-                            __hip_atomic_store(&C.exhausted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_sub(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            state = -1;
-                        } else {
-                            C.g_tile[g] = unit_t;
-                            C.g_uc[g] = unit_uc;
-                            const int cs0 = s_begin + unit_uc * P.chunk;
-                            C.g_cs1[g] = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
-                            if (unit_uc > 0 &&
-                                __hip_atomic_load(A.tile_done + unit_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unit_uc) {
-                                // its tile's previous chunk is not published yet: start it later
-                                __hip_atomic_store(&C.g_left[g], -2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                state = -2;
-                            }
+        // this wave holds no query: start a group, shade, or wait
+        int gsel = -1;
+        if (attn) {  // a group to start: an idle one while units remain, or one whose tile is ready
+            if (lane == 0) {
+                for (int g = 0; g < G && gsel < 0; g++) {
+                    if (!((attn >> g) & 1)) continue;
+                    const int gl = lds_ld(&C.g_left[g]);
+                    int expect = gl;
+                    if (gl == -2) {
+                        if (__hip_atomic_load(A.tile_done + C.g_tile[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= C.g_uc[g] &&
+                            __hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
+                            gsel = g;
+                    } else if (gl == -1) {
+                        if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -4, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                            gsel = g;
+                            __hip_atomic_fetch_add(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     }
+                    if (gsel >= 0) __hip_atomic_fetch_and(&C.attn, ~(1u << g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                state = __builtin_amdgcn_readfirstlane(state);
-                if (state == -1 || state == -2) continue;
-                lds_order();
-                const int ut = C.g_tile[g], uc = C.g_uc[g];
-                if (uc > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's running means
-                const int i = (ut % tiles_x) * 8 + (lane & 7), j = (ut / tiles_x) * 8 + (lane >> 3);
-                const bool in_image = i < P.width && j < P.height;
-                const int s = g * 64 + lane;
-                const int cs0 = s_begin + uc * P.chunk;
-                const int pixel = j * P.width + i;
-                if (in_image) {
-                    const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
-                    WfAcc acc{im, V3(al.x, al.y, al.z), V3(nr.x, nr.y, nr.z), 0, 1.0f / (float)(cs0 - P.first + 1)};
-                    Path st;
-                    start_path(P, i, j, pixel, cs0, st);
-                    wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0, acc);
-                    issue(s, st);
-                    pend = s;
-                }
-                const int started = lane_count(__builtin_amdgcn_ballot_w64(in_image));
-                if (lane == 0) __hip_atomic_store(&C.g_left[g], started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                WF_STAMP(2);
-                continue;
             }
-            // shade when a full batch waits, or when the traversal waves are about to run dry
-            if (!(sl >= (unsigned)P.wait_lanes || (sl > 0 && tl < (unsigned)P.wf_refill * 4))) {
-                if (sl == 0 && tl == 0 && finished_all()) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (++idle_iters > (1u << 27)) {  // bounded: never expected
-                    if (lane == 0) atomicAdd(A.counters + 7, 1ull);
-                    break;
-                }
-                WF_STAMP(3);
-                continue;
-            }
-            idle_iters = 0;
-            // ------------------------------------------------------------ shade a batch
-            unsigned base;
-            const int n = wf_claim(C, WF_SCENE, 64, base);
-            if (n == 0) continue;
-            WF_ADD(7, 1);
-            WF_ADD(8, n);
-            const bool mine = lane < n;
-            int s = -1;
-            bool alive = false;
-            if (mine) {
-                s = wf_take(C, ring[WF_SCENE], (base + (unsigned)lane) % (unsigned)NP);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                Path st;
-                WfAcc acc;
-                int pixel, sample;
-                wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
-                const float4 hh = r_h[s];
-                const Hit h{__float_as_int(hh.x), __float_as_int(hh.y), hh.z, hh.w, r_t[s], __float_as_int(hh.x) >= 0};
-                const WfAov aov{&acc};
-                bool done;
-                if (SAMPLER == 2) done = naive_hit<F>(S, P, st, h, aov, cnt.shades);
-                else done = path_hit<F>(S, P, st, h, aov, cnt.shades);
-                // sample_lights_pdf's instance queries, inline (src/trace.jl:1018-1044)
-                while (SAMPLER == 1 && !done && st.phase == PH_LIGHT) {
-                    cnt.light_queries++;
-                    query_begin(T, st.lq, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
-                    while (T.sp > 0 || T.nprim > 0) {
-                        if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-                        else node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
+            gsel = __builtin_amdgcn_readfirstlane(gsel);
+        }
+        WF_STAMP(14);
+        WF_ADD(13, 1);
+        if (gsel >= 0) {
+            // ------------------------------------------------------------ start a slot group
+            const int g = gsel;
+            int state = 0;
+            if (lane == 0) {
+                state = C.g_left[g];
+                if (state == -4) {  // idle group: fetch a unit (this XCD's band first, then the others)
+                    int unit_uc = -1, unit_t = 0;
+                    for (;;) {
+                        const int bk = lds_ld(&C.band_k);
+                        if (bk >= NBANDS) break;
+                        const int band = (int)((xcc + (unsigned)bk) & (NBANDS - 1));
+                        const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
+                        const unsigned unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
+                        if (unit < (unsigned)bn * (unsigned)nchunks) {
+                            unit_uc = (int)(unit / (unsigned)bn);
+                            unit_t = bt0 + (int)(unit % (unsigned)bn);
+                            break;
+                        }
+                        int expect = bk;
+                        __hip_atomic_compare_exchange_strong(&C.band_k, &expect, bk + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    done = light_hit<F>(S, P, st, query_hit(T));
-                }
-                alive = true;
-                if (done) {
-                    // trace_sample's epilogue (src/trace.jl:625-648) on the slot's running means
-                    cnt.paths++;
-                    v3 radiance = st.radiance;
-                    if (!all_finite(radiance)) radiance = V3(0, 0, 0);
-                    const float mr = max3(radiance);
-                    if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
-                    const float w = acc.w;
-                    const float omw = 1 - w;
-                    const bool hit = st.flags & F_HIT;
-                    const bool env = !hit && !P.envhidden && S.nenvs != 0;
-                    const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
-                    if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
-                    acc.im.x = acc.im.x * omw + target.x * w;
-                    acc.im.y = acc.im.y * omw + target.y * w;
-                    acc.im.z = acc.im.z * omw + target.z * w;
-                    acc.im.w = acc.im.w * omw + target.w * w;
-                    if (hit || env) acc.hits += 1;
-                    if (++sample < C.g_cs1[s >> 6]) {
-                        acc.w = 1.0f / (float)(sample - P.first + 1);
-                        start_path(P, pixel % P.width, pixel / P.width, pixel, sample, st);
-                    } else {  // the slot's chunk is done: its pixel's running means back to HBM
-                        alive = false;
-                        A.image[pixel] = acc.im;
-                        A.albedo[pixel] = make_float4(acc.al.x, acc.al.y, acc.al.z, 0.0f);
-                        A.normal[pixel] = make_float4(acc.nr.x, acc.nr.y, acc.nr.z, 0.0f);
-                        A.hits[pixel] += acc.hits;
-                    }
-                }
-                if (alive) {
-                    wf_store<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
-                    issue(s, st);
-                    pend = s;
-                }
-            }
-            // slots whose chunk is done: the last one of its group publishes the tile
-            const bool fin = mine && !alive;
-            if (__builtin_amdgcn_ballot_w64(fin)) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                bool last = false;
-                const int g = s >> 6;
-                if (fin) last = __hip_atomic_fetch_add(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 1;
-                if (__builtin_amdgcn_ballot_w64(last)) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                    if (last) {
-                        if (C.g_uc[g] + 1 < nchunks)
-                            __hip_atomic_store(A.tile_done + C.g_tile[g], C.g_uc[g] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (unit_uc < 0) {  // no units left: this group stays idle
+                        __hip_atomic_store(&C.exhausted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (!lds_ld(&C.exhausted))
-                            __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_fetch_sub(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        state = -1;
+                    } else {
+                        C.g_tile[g] = unit_t;
+                        C.g_uc[g] = unit_uc;
+                        const int cs0 = s_begin + unit_uc * P.chunk;
+                        C.g_cs1[g] = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
+                        if (unit_uc > 0 &&
+                            __hip_atomic_load(A.tile_done + unit_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unit_uc) {
+                            // its tile's previous chunk is not published yet: start it later
+                            __hip_atomic_store(&C.g_left[g], -2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            state = -2;
+                        }
                     }
                 }
             }
-            WF_STAMP(1);
+            state = __builtin_amdgcn_readfirstlane(state);
+            if (state == -1 || state == -2) continue;
+            lds_order();
+            const int ut = C.g_tile[g], uc = C.g_uc[g];
+            if (uc > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's running means
+            const int i = (ut % tiles_x) * 8 + (lane & 7), j = (ut / tiles_x) * 8 + (lane >> 3);
+            const bool in_image = i < P.width && j < P.height;
+            const int s = g * 64 + lane;
+            const int cs0 = s_begin + uc * P.chunk;
+            const int pixel = j * P.width + i;
+            if (in_image) {
+                const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
+                WfAcc acc{im, V3(al.x, al.y, al.z), V3(nr.x, nr.y, nr.z), 0, 1.0f / (float)(cs0 - P.first + 1)};
+                Path st;
+                start_path(P, i, j, pixel, cs0, st);
+                wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0, acc);
+                issue(s, st);
+                pend = s;
+            }
+            const int started = lane_count(__builtin_amdgcn_ballot_w64(in_image));
+            if (lane == 0) __hip_atomic_store(&C.g_left[g], started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            WF_STAMP(2);
+            continue;
         }
+        // a shading wave shades when a full batch waits or the traversal waves are about to run
+        // dry; a traversal wave without queries shades whatever waits
+        if (!(sl >= (unsigned)P.wait_lanes || (sl > 0 && (!shader || tl < (unsigned)P.wf_refill * 4)))) {
+            if (sl == 0 && tl == 0 && finished_all()) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++idle_iters > (1u << 27)) {  // bounded: never expected
+                if (lane == 0) atomicAdd(A.counters + 7, 1ull);
+                break;
+            }
+            WF_STAMP(3);
+            continue;
+        }
+        idle_iters = 0;
+        // ------------------------------------------------------------ shade a batch
+        unsigned base;
+        const int n = wf_claim(C, WF_SCENE, 64, base);
+        if (n == 0) continue;
+        WF_ADD(7, 1);
+        WF_ADD(8, n);
+        const bool mine = lane < n;
+        int s = -1;
+        bool alive = false;
+        if (mine) {
+            s = wf_take(C, ring[WF_SCENE], (base + (unsigned)lane) % (unsigned)NP);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            Path st;
+            WfAcc acc;
+            int pixel, sample;
+            wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
+            const float4 hh = r_h[s];
+            const Hit h{__float_as_int(hh.x), __float_as_int(hh.y), hh.z, hh.w, r_t[s], __float_as_int(hh.x) >= 0};
+            const WfAov aov{&acc};
+            bool done;
+            if (SAMPLER == 2) done = naive_hit<F>(S, P, st, h, aov, cnt.shades);
+            else done = path_hit<F>(S, P, st, h, aov, cnt.shades);
+            // sample_lights_pdf's instance queries, inline (src/trace.jl:1018-1044)
+            while (SAMPLER == 1 && !done && st.phase == PH_LIGHT) {
+                cnt.light_queries++;
+                query_begin(T, st.lq, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
+                while (T.sp > 0 || T.nprim > 0) {
+                    if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+                    else node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
+                }
+                done = light_hit<F>(S, P, st, query_hit(T));
+            }
+            alive = true;
+            if (done) {
+                // trace_sample's epilogue (src/trace.jl:625-648) on the slot's running means
+                cnt.paths++;
+                v3 radiance = st.radiance;
+                if (!all_finite(radiance)) radiance = V3(0, 0, 0);
+                const float mr = max3(radiance);
+                if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
+                const float w = acc.w;
+                const float omw = 1 - w;
+                const bool hit = st.flags & F_HIT;
+                const bool env = !hit && !P.envhidden && S.nenvs != 0;
+                const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
+                if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
+                acc.im.x = acc.im.x * omw + target.x * w;
+                acc.im.y = acc.im.y * omw + target.y * w;
+                acc.im.z = acc.im.z * omw + target.z * w;
+                acc.im.w = acc.im.w * omw + target.w * w;
+                if (hit || env) acc.hits += 1;
+                if (++sample < C.g_cs1[s >> 6]) {
+                    acc.w = 1.0f / (float)(sample - P.first + 1);
+                    start_path(P, pixel % P.width, pixel / P.width, pixel, sample, st);
+                } else {  // the slot's chunk is done: its pixel's running means back to HBM
+                    alive = false;
+                    A.image[pixel] = acc.im;
+                    A.albedo[pixel] = make_float4(acc.al.x, acc.al.y, acc.al.z, 0.0f);
+                    A.normal[pixel] = make_float4(acc.nr.x, acc.nr.y, acc.nr.z, 0.0f);
+                    A.hits[pixel] += acc.hits;
+                }
+            }
+            if (alive) {
+                wf_store<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
+                issue(s, st);
+                pend = s;
+            }
+        }
+        // slots whose chunk is done: the last one of its group publishes the tile
+        const bool fin = mine && !alive;
+        if (__builtin_amdgcn_ballot_w64(fin)) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            bool last = false;
+            const int g = s >> 6;
+            if (fin) last = __hip_atomic_fetch_add(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 1;
+            if (__builtin_amdgcn_ballot_w64(last)) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                if (last) {
+                    if (C.g_uc[g] + 1 < nchunks)
+                        __hip_atomic_store(A.tile_done + C.g_tile[g], C.g_uc[g] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (!lds_ld(&C.exhausted))
+                        __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_sub(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+        WF_STAMP(1);
     }
 #if JT_STAMPS
     if (lane == 0)

@@ -8,7 +8,7 @@ scripts/gpu_step.sh 300 $O/pytest_wf.log timeout -k 10 280 python -u -m pytest t
 grep -q " passed" $O/pytest_wf.log || exit 1
 grep -q "failed" $O/pytest_wf.log && exit 1
 scripts/gpu_step.sh 120 $O/bench_mk.log timeout -k 10 100 python bench.py --no-cpu-baseline --steps 2 || exit 1
-for cfg in ${WF_CFGS:-"5 56 8 1" "5 32 8 1" "5 56 8 2" "8 56 8 1" "8 32 8 1" "8 56 16 1" "4 48 8 1"}; do
+for cfg in "5 56 8 1" "5 40 8 1" "5 64 8 1" "5 56 8 2" "6 56 8 1" "4 56 8 1" "5 56 16 1" "5 56 4 1"; do
   set -- $cfg
   JT_WF=1 JT_WF_GROUPS=$1 JT_WAIT_LANES=$2 JT_WF_REFILL=$3 JT_WF_SHADERS=$4 scripts/gpu_step.sh 120 $O/bench_wf_g$1_w$2_r$3_s$4.log timeout -k 10 100 python bench.py --no-cpu-baseline --steps 2 || exit 1
 done
