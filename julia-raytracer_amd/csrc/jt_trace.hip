@@ -1208,10 +1208,10 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 // shading on full batches. Each path's float operations and RNG draws are the reference's, in
 // its order, and a pixel's samples are accumulated in order (one slot per pixel and chunk; the
 // chunks of a tile in order): results are bit-identical to trace_body.
-constexpr int WF_GMAX = 16;
-constexpr int WF_TRAV = 0, WF_SCENE = 1;
+constexpr int WF_GMAX = 8;
+constexpr int WF_TRAV = 0, WF_SCENE = 1, WF_LIGHT = 2;
 struct WfCtl {
-    unsigned head[3], tail[3];  // ring cursors (traversal, scene results; [2] unused)
+    unsigned head[3], tail[3];  // ring cursors
     unsigned attn;              // groups a wave should look at: idle while units remain, or waiting on a tile
     unsigned live;              // groups holding (or claiming) a unit
     int g_tile[WF_GMAX], g_uc[WF_GMAX], g_cs1[WF_GMAX];
@@ -1220,10 +1220,8 @@ struct WfCtl {
     int exhausted;  // every band's units handed out
     int abort;      // a ring entry never arrived (never expected): every wave leaves, the launch fails
 };
-// float4s per slot record: path state (8), running means (2.5) + the query's hit (1.5), the volume (2, FT_VOL)
-__host__ __device__ constexpr int wf_rec_q(int F) { return (F & FT_VOL) ? 14 : 12; }
-// LDS bytes per slot: two ring entries and the pending query (origin, direction)
-constexpr int WF_LDS_SLOT = 2 * 4 + 16 + 8;
+// float4s per slot record: path state (8), running means (3), the volume (2, FT_VOL)
+__host__ __device__ constexpr int wf_rec_q(int F) { return (F & FT_VOL) ? 13 : 11; }
 struct WfAcc {  // a slot's pixel running means (trace_body's acc slots), in registers while it shades
     float4 im;
     v3 al, nr;
@@ -1245,22 +1243,16 @@ __device__ __forceinline__ void wf_store(float4* r, const Path& st, int pixel, i
     r[7] = make_float4(__int_as_float(pixel), __int_as_float(sample), a.w, __int_as_float(a.hits));
     r[8] = a.im;
     r[9] = make_float4(a.al.x, a.al.y, a.al.z, a.nr.x);
-    reinterpret_cast<float2*>(r + 10)[0] = make_float2(a.nr.y, a.nr.z);  // .zw: the hit (wf_store_hit)
+    r[10] = make_float4(a.nr.y, a.nr.z, 0.0f, 0.0f);
     if (F & FT_VOL) {
-        r[12] = make_float4(st.vol.density.x, st.vol.density.y, st.vol.density.z, st.vol.scattering.x);
-        r[13] = make_float4(st.vol.scattering.y, st.vol.scattering.z, st.vol.scanisotropy, 0.0f);
+        r[11] = make_float4(st.vol.density.x, st.vol.density.y, st.vol.density.z, st.vol.scattering.x);
+        r[12] = make_float4(st.vol.scattering.y, st.vol.scattering.z, st.vol.scanisotropy, 0.0f);
     }
 }
-// the closest hit of the slot's scene query, written by the lane that traversed it
-__device__ __forceinline__ void wf_store_hit(float4* r, const Trav& T) {
-    reinterpret_cast<float2*>(r + 10)[1] = make_float2(__int_as_float(T.h_inst), __int_as_float(T.h_elem));
-    r[11] = make_float4(T.h_u, T.h_v, T.tmax, 0.0f);
-}
 template <int F>
-__device__ __forceinline__ void wf_load(const float4* r, Path& st, int& pixel, int& sample, WfAcc& a, Hit& h) {
+__device__ __forceinline__ void wf_load(const float4* r, Path& st, int& pixel, int& sample, WfAcc& a) {
     const float4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6], q7 = r[7];
-    const float4 q8 = r[8], q9 = r[9], q10 = r[10], q11 = r[11];
-    h = Hit{__float_as_int(q10.z), __float_as_int(q10.w), q11.x, q11.y, q11.z, __float_as_int(q10.z) >= 0};
+    const float4 q8 = r[8], q9 = r[9], q10 = r[10];
     st.o = V3(q0.x, q0.y, q0.z);
     st.d = V3(q0.w, q1.x, q1.y);
     st.radiance = V3(q1.z, q1.w, q2.x);
@@ -1286,7 +1278,7 @@ __device__ __forceinline__ void wf_load(const float4* r, Path& st, int& pixel, i
     a.al = V3(q9.x, q9.y, q9.z);
     a.nr = V3(q9.w, q10.x, q10.y);
     if (F & FT_VOL) {
-        const float4 v0 = r[12], v1 = r[13];
+        const float4 v0 = r[11], v1 = r[12];
         st.vol.density = V3(v0.x, v0.y, v0.z);
         st.vol.scattering = V3(v0.w, v1.x, v1.y);
         st.vol.scanisotropy = v1.z;
@@ -1381,9 +1373,11 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     const int lane = threadIdx.x & 63;
     const int G = P.wf_groups, NP = 64 * G;
     __shared__ WfCtl C;
-    int* const ring[2] = {lds_wf, lds_wf + NP};
-    float4* const q_a = reinterpret_cast<float4*>(lds_wf + 2 * NP);  // pending scene query: o.xyz, d.x
-    float2* const q_b = reinterpret_cast<float2*>(q_a + NP);         // d.yz
+    int* const ring[3] = {lds_wf, lds_wf + NP, lds_wf + 2 * NP};
+    float4* const q_o = reinterpret_cast<float4*>(lds_wf + 3 * NP);  // o.xyz, root bits
+    float4* const q_d = q_o + NP;                                       // d.xyz
+    float4* const r_h = q_d + NP;                                       // inst, elem, u, v
+    float* const r_t = reinterpret_cast<float*>(r_h + NP);              // t
     float4* const recs = pool + (size_t)blockIdx.x * NP * RQ;
     if (threadIdx.x < 3) {
         C.head[threadIdx.x] = 0;
@@ -1397,7 +1391,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
         C.exhausted = 0;
         C.abort = 0;
     }
-    for (int k = threadIdx.x; k < 2 * NP; k += BLOCK) lds_wf[k] = -1;
+    for (int k = threadIdx.x; k < 3 * NP; k += BLOCK) lds_wf[k] = -1;
     __syncthreads();
 
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
@@ -1409,7 +1403,6 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     T.sp = 0;
     T.nprim = 0;
     int qslot = -1;  // the slot whose query this lane runs (-1: none)
-    int rpend = -1;  // a slot whose hit this lane stored, waiting to be pushed for shading
     int pend = -1;   // a slot this lane shaded whose next query waits to be pushed (after its record store)
     unsigned idle_iters = 0;
 #if JT_STAMPS
@@ -1423,19 +1416,16 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
 #define WF_ADD(k, v) ((void)0)
 #endif
 
-    // a slot's pending closest-hit scene query (LDS): origin, direction
+    // a slot's pending query (LDS): origin, direction, root
     auto issue = [&](int s, const Path& st) {
-        q_a[s] = make_float4(st.o.x, st.o.y, st.o.z, st.d.x);
-        q_b[s] = make_float2(st.d.y, st.d.z);
-        cnt.rays++;
-    };
-    // hits stored by this wave's lanes: publish them for shading (after the stores)
-    auto flush_hits = [&]() {
-        if (__builtin_amdgcn_ballot_w64(rpend >= 0)) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            wf_push(C, ring[WF_SCENE], NP, WF_SCENE, rpend >= 0, rpend);
-            rpend = -1;
-        }
+        const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
+        const v3 o = light ? st.lq : st.o;
+        const unsigned root = light ? (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance
+                                    : (T_TLAS << 30) | SNAP_NONE;
+        q_o[s] = make_float4(o.x, o.y, o.z, __uint_as_float(root));
+        q_d[s] = make_float4(st.d.x, st.d.y, st.d.z, 0.0f);
+        if (light) cnt.light_queries++;
+        else cnt.rays++;
     };
 
     // Roles: the last P.wf_shaders waves of the workgroup only shade and start slot groups; the
@@ -1480,10 +1470,9 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                         const int r = lane_rank(__builtin_amdgcn_ballot_w64(qslot < 0));
                         if (qslot < 0 && r < n) {
                             const int s = wf_take(C, ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
-                            const float4 a = q_a[s];
-                            const float2 b = q_b[s];
+                            const float4 o = q_o[s], d = q_d[s];
                             qslot = s;
-                            query_begin(T, V3(a.x, a.y, a.z), V3(a.w, b.x, b.y), (T_TLAS << 30) | SNAP_NONE, stack);
+                            query_begin(T, V3(o.x, o.y, o.z), V3(d.x, d.y, d.z), __float_as_uint(o.w), stack);
 #pragma unroll
                             for (int k = 0; k < JT_FIRST_POP; k++)
                                 if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
@@ -1504,21 +1493,22 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                     for (int k = 0; k < JT_NODE_REPEAT; k++)
                         if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
                 }
-                // finished queries: the hit into the slot record; the slot goes onto the shading
-                // ring one iteration later, when the store has completed
-                flush_hits();
+                // finished queries: the result to LDS, the slot onto the shading ring
                 const bool fin = qslot >= 0 && (T.sp | T.nprim) == 0;
-                if (fin) {
-                    wf_store_hit(recs + (size_t)qslot * RQ, T);
-                    rpend = qslot;
-                    qslot = -1;
+                if (__builtin_amdgcn_ballot_w64(fin)) {
+                    if (fin) {
+                        r_h[qslot] = make_float4(__int_as_float(T.h_inst), __int_as_float(T.h_elem), T.h_u, T.h_v);
+                        r_t[qslot] = T.tmax;
+                    }
+                    lds_order();
+                    wf_push(C, ring[WF_SCENE], NP, WF_SCENE, fin, qslot);
+                    if (fin) qslot = -1;
                 }
                 busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
                 cv = ctl();
                 tq = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
                 if (busy == 0 && tq == 0) break;
             }
-            flush_hits();
             WF_STAMP(0);
             continue;
         }
@@ -1644,8 +1634,9 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             Path st;
             WfAcc acc;
             int pixel, sample;
-            Hit h;
-            wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample, acc, h);
+            wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
+            const float4 hh = r_h[s];
+            const Hit h{__float_as_int(hh.x), __float_as_int(hh.y), hh.z, hh.w, r_t[s], __float_as_int(hh.x) >= 0};
             const WfAov aov{&acc};
             bool done;
             if (SAMPLER == 2) done = naive_hit<F>(S, P, st, h, aov, cnt.shades);
@@ -1820,7 +1811,7 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_WF void trace_kernel_wf(DSce
     const int NP = 64 * P.wf_groups;
     int* const stack = reinterpret_cast<int*>(dyn_lds);
     int* const wf = stack + S.stack_need * BLOCK;
-    uint4* const blob = reinterpret_cast<uint4*>(reinterpret_cast<char*>(wf) + (size_t)NP * WF_LDS_SLOT);
+    uint4* const blob = reinterpret_cast<uint4*>(wf + 3 * NP) + 3 * NP + NP / 4;
     DScene L = S;
     if (LDSM) {
         for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
@@ -1865,7 +1856,8 @@ template <int SAMPLER, int COUNT, int F>
 hipError_t launch_wf(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
     const int NP = 64 * P.wf_groups;
     const bool ldsm = S.blob_n16 > 0;
-    const size_t lds = (size_t)S.stack_need * BLOCK * 4 + (size_t)NP * WF_LDS_SLOT + (ldsm ? (size_t)S.blob_n16 * 16 : 0);
+    const size_t lds = (size_t)S.stack_need * BLOCK * 4 + (size_t)NP * (3 * 4 + 3 * 16 + 4) +
+                       (ldsm ? (size_t)S.blob_n16 * 16 : 0);
     const void* k = ldsm ? (const void*)trace_kernel_wf<SAMPLER, COUNT, F, true>
                          : (const void*)trace_kernel_wf<SAMPLER, COUNT, F, false>;
     hipError_t e;
@@ -2592,7 +2584,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.wf_groups = 0;
     if (const char* wf = std::getenv("JT_WF")) {
         if (std::atoi(wf) > 0 && c->stack <= 16) {
-            P.wf_groups = 10;
+            P.wf_groups = 6;
             if (const char* g = std::getenv("JT_WF_GROUPS")) P.wf_groups = std::max(1, std::min(WF_GMAX, std::atoi(g)));
             P.wait_lanes = 56;
             if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
