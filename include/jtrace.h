@@ -257,6 +257,17 @@ int jt_image_size(const jt_scene* scene, const jt_params* params, int32_t* width
  * environment lights (src/trace.jl:1003). */
 int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
               const jt_params* params, jt_ctx** out);
+/* jt_create over several GPUs of one node (SURVEY §8(b) "jt_create(..., num_devices, ...)"; the
+ * reference's caller is Jtrace.main's batch loop, src/jtrace.jl:83-106). devices: ndevices
+ * distinct HIP ordinals, or NULL for 0 .. ndevices-1 (params->device is ignored). Every other
+ * function takes the returned context: jt_trace_range / jt_trace_samples split each batch into
+ * contiguous per-device shares, traced concurrently, each device keeping its own running mean
+ * over its samples; jt_get_image / jt_get_aovs reduce them onto device 0 with one RCCL reduce
+ * (sum of mean_d * n_d / N; hits summed), so the image equals the single-device one up to fp32
+ * summation order. jt_get_counters sums the devices (kernel_ms: per launch the slowest device);
+ * jt_get_device_buffers returns device 0's share. */
+int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
+                    const jt_params* params, const int32_t* devices, int32_t ndevices, jt_ctx** out);
 /* trace_samples (src/trace.jl:215-274): samples [n, min(n+batch, samples)), n += batch. */
 int jt_trace_samples(jt_ctx* ctx);
 /* Accumulate global samples [sample_begin, sample_end) into the running mean, in order.

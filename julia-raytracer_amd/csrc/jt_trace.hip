@@ -14,6 +14,7 @@
 // mean (lerp with w = 1/(s+1), src/trace.jl:631-648) is kept in registers across samples and
 // written once per launch.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -1950,12 +1951,23 @@ struct jt_ctx {
     size_t lds_scene_bytes = 0;  // > 0: small-scene LDS mode
     unsigned long long launches = 0;
     double kernel_ms = 0;
+    // multi-device context (jt_create_multi): one sub-context per device, each tracing its share
+    // of every batch into its own running mean; RCCL communicators for the reduce of jt_get_image
+    std::vector<jt_ctx*> sub;
+    std::vector<ncclComm_t> comms;
+    std::vector<long long> nsub;  // samples accumulated by each device
+    float* red = nullptr;         // device 0: reduce target, W*H float4
+    long long* red_hits = nullptr;
 };
 
 namespace {
 
 int hip_fail(hipError_t e, const char* what) {
     return jt::fail(JT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int nccl_fail(ncclResult_t r, const char* what) {
+    return jt::fail(JT_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
 template <class T>
@@ -2057,6 +2069,17 @@ int jt_device_count(int32_t* out) {
 
 void jt_destroy(jt_ctx* c) {
     if (!c) return;
+    if (!c->sub.empty() || !c->comms.empty()) {
+        for (ncclComm_t m : c->comms) (void)ncclCommDestroy(m);
+        if (!c->sub.empty()) {
+            (void)hipSetDevice(c->sub[0]->device);
+            if (c->red) (void)hipFree(c->red);
+            if (c->red_hits) (void)hipFree(c->red_hits);
+        }
+        for (jt_ctx* s : c->sub) jt_destroy(s);
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocations) (void)hipFree(p);
@@ -2584,7 +2607,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.wf_groups = 0;
     if (const char* wf = std::getenv("JT_WF")) {
         if (std::atoi(wf) > 0 && c->stack <= 16) {
-            P.wf_groups = 6;
+            P.wf_groups = 5;
             if (const char* g = std::getenv("JT_WF_GROUPS")) P.wf_groups = std::max(1, std::min(WF_GMAX, std::atoi(g)));
             P.wait_lanes = 56;
             if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
@@ -2632,8 +2655,74 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     return JT_OK;
 }
 
+int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights, const jt_params* params,
+                    const int32_t* devices, int32_t ndevices, jt_ctx** out) {
+    if (!out) return jt::fail(JT_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (!params) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    int avail = 0;
+    if (hipGetDeviceCount(&avail) != hipSuccess) avail = 0;
+    if (ndevices < 1 || ndevices > avail)
+        return jt::fail(JT_ERR_INVALID, "ndevices must be in [1, " + std::to_string(avail) + "]");
+    std::vector<int> devs(ndevices);
+    for (int d = 0; d < ndevices; d++) {
+        devs[d] = devices ? devices[d] : d;
+        if (devs[d] < 0 || devs[d] >= avail) return jt::fail(JT_ERR_INVALID, "device id out of range");
+        for (int k = 0; k < d; k++)
+            if (devs[k] == devs[d]) return jt::fail(JT_ERR_INVALID, "a device is listed twice");
+    }
+    jt_ctx* c = new jt_ctx();
+    for (int d = 0; d < ndevices; d++) {
+        jt_params p = *params;
+        p.device = devs[d];
+        jt_ctx* s = nullptr;
+        const int st = jt_create(scene, bvh, lights, &p, &s);
+        if (st != JT_OK) {
+            jt_destroy(c);
+            return st;
+        }
+        c->sub.push_back(s);
+    }
+    c->nsub.assign(ndevices, 0);
+    c->comms.resize(ndevices);
+    ncclResult_t r = ncclCommInitAll(c->comms.data(), ndevices, devs.data());
+    if (r != ncclSuccess) {
+        c->comms.clear();
+        jt_destroy(c);
+        return nccl_fail(r, "ncclCommInitAll");
+    }
+    jt_ctx* s0 = c->sub[0];
+    c->device = s0->device;
+    c->width = s0->width;
+    c->height = s0->height;
+    c->total_samples = s0->total_samples;
+    c->batch = s0->batch;
+    c->sampler = s0->sampler;
+    (void)hipSetDevice(s0->device);
+    const size_t np = (size_t)c->width * c->height;
+    if (hipMalloc(&c->red, np * 16) != hipSuccess || hipMalloc(&c->red_hits, np * 8) != hipSuccess) {
+        jt_destroy(c);
+        return jt::fail(JT_ERR_NOMEM, "hipMalloc reduce buffers");
+    }
+    *out = c;
+    return JT_OK;
+}
+
 int jt_reset(jt_ctx* c) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    if (!c->sub.empty()) {
+        for (jt_ctx* s : c->sub) {
+            const int st = jt_reset(s);
+            if (st != JT_OK) return st;
+        }
+        std::fill(c->nsub.begin(), c->nsub.end(), 0LL);
+        c->first = -1;
+        c->next = 0;
+        c->failed = false;
+        c->launches = 0;
+        c->kernel_ms = 0;
+        return JT_OK;
+    }
     (void)hipSetDevice(c->device);
     const size_t np = (size_t)c->width * (size_t)c->height;
     hipError_t e;
@@ -2652,15 +2741,12 @@ int jt_reset(jt_ctx* c) {
     return JT_OK;
 }
 
-int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
-    if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
-    if (s0 < 0 || s1 < s0) return jt::fail(JT_ERR_STATE, "invalid sample range");
-    if (s0 == s1) return JT_OK;
-    if (c->failed) return jt::fail(JT_ERR_STATE, "a previous launch failed; jt_reset the context");
-    if (c->first >= 0 && s0 != c->next)
-        return jt::fail(JT_ERR_STATE, "samples must be accumulated in order (expected " + std::to_string(c->next) + ")");
-    if (c->first < 0) c->first = s0;
-    c->P.first = c->first;
+}  // extern "C"
+
+namespace {
+// enqueue one launch over global samples [s0, s1) whose running-mean weight is 1/(s - first + 1)
+int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
+    c->P.first = first;
     c->P.chunk = c->chunk > 0 ? c->chunk : std::max(8, std::min(64, (s1 - s0) / 4));
     (void)hipSetDevice(c->device);
     hipError_t e = hipMemsetAsync(c->A.work, 0, (size_t)(c->tiles + NBANDS * BAND_STRIDE) * 4, c->stream);
@@ -2676,18 +2762,126 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
                      : launch_s<1, 0>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    return JT_OK;
+}
+// wait for the launch; its device time in *ms
+int trace_finish(jt_ctx* c, float* ms) {
+    (void)hipSetDevice(c->device);
+    hipError_t e;
     if ((e = hipEventSynchronize(c->ev1)) != hipSuccess) return hip_fail(e, "trace kernel");
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
-    c->kernel_ms += ms;
+    *ms = 0;
+    (void)hipEventElapsedTime(ms, c->ev0, c->ev1);
+    c->kernel_ms += *ms;
     c->launches++;
-    c->next = s1;
     unsigned long long timeouts = 0;
     if ((e = hipMemcpy(&timeouts, c->A.counters + 7, 8, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
     if (timeouts) {  // a wave accumulated without its predecessor chunk: the means are corrupt
         c->failed = true;
         return jt::fail(JT_ERR_DEVICE, "work-unit ordering wait timed out");
     }
+    return JT_OK;
+}
+
+// multi-device trace_samples step: [s0, s1) split into contiguous shares, one per device, each
+// appended to that device's own running mean (weight 1/(n_d + k + 1) for its k-th new sample)
+int multi_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
+    const int D = (int)c->sub.size();
+    const long long L = s1 - s0;
+    std::vector<int> a(D), b(D);
+    for (int d = 0; d < D; d++) {
+        a[d] = s0 + (int)(L * d / D);
+        b[d] = s0 + (int)(L * (d + 1) / D);
+        if (a[d] < b[d]) {
+            int st = trace_launch(c->sub[d], a[d], b[d], (int32_t)(a[d] - c->nsub[d]));
+            if (st != JT_OK) return st;
+        }
+    }
+    float wall = 0;
+    int status = JT_OK;
+    for (int d = 0; d < D; d++) {
+        if (a[d] >= b[d]) continue;
+        float ms = 0;
+        const int st = trace_finish(c->sub[d], &ms);
+        if (st != JT_OK && status == JT_OK) status = st;
+        c->nsub[d] += b[d] - a[d];
+        wall = std::max(wall, ms);
+    }
+    if (status != JT_OK) {
+        c->failed = true;
+        return status;
+    }
+    c->kernel_ms += wall;  // the launches run concurrently: the slowest device's time
+    c->launches++;
+    c->next = s1;
+    return JT_OK;
+}
+
+// the sample-weighted reduce of the devices' running means onto device 0 (one RCCL reduce with a
+// per-rank premultiplied sum: sum_d mean_d * n_d / N), then to the host. which: 0 image, 1
+// albedo, 2 normal (float4 buffers); hits (int64) are summed.
+int multi_reduce(jt_ctx* c, int which, float* out4, int64_t* hits) {
+    const int D = (int)c->sub.size();
+    const size_t np = (size_t)c->width * c->height;
+    long long N = 0;
+    for (long long n : c->nsub) N += n;
+    std::vector<ncclRedOp_t> ops(D);
+    std::vector<float> w(D);
+    ncclResult_t r;
+    if (out4) {
+        for (int d = 0; d < D; d++) {
+            w[d] = N > 0 ? (float)((double)c->nsub[d] / (double)N) : (d == 0 ? 1.0f : 0.0f);
+            if ((r = ncclRedOpCreatePreMulSum(&ops[d], &w[d], ncclFloat32, ncclScalarHostImmediate, c->comms[d])) != ncclSuccess)
+                return nccl_fail(r, "ncclRedOpCreatePreMulSum");
+        }
+    }
+    if ((r = ncclGroupStart()) != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
+    for (int d = 0; d < D; d++) {
+        jt_ctx* s = c->sub[d];
+        (void)hipSetDevice(s->device);
+        if (out4) {
+            const float4* src = which == 0 ? s->A.image : which == 1 ? s->A.albedo : s->A.normal;
+            r = ncclReduce(src, d == 0 ? (void*)c->red : (void*)src, np * 4, ncclFloat32, ops[d], 0, c->comms[d], s->stream);
+        } else {
+            r = ncclReduce(s->A.hits, d == 0 ? (void*)c->red_hits : (void*)s->A.hits, np, ncclInt64, ncclSum, 0, c->comms[d],
+                           s->stream);
+        }
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();
+            return nccl_fail(r, "ncclReduce");
+        }
+    }
+    if ((r = ncclGroupEnd()) != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
+    hipError_t e;
+    for (int d = 0; d < D; d++) {
+        (void)hipSetDevice(c->sub[d]->device);
+        if ((e = hipStreamSynchronize(c->sub[d]->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    }
+    if (out4)
+        for (int d = 0; d < D; d++) (void)ncclRedOpDestroy(ops[d], c->comms[d]);
+    (void)hipSetDevice(c->sub[0]->device);
+    if (out4) e = hipMemcpy(out4, c->red, np * 16, hipMemcpyDeviceToHost);
+    else e = hipMemcpy(hits, c->red_hits, np * 8, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy reduce");
+}
+}  // namespace
+
+extern "C" {
+
+int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
+    if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    if (s0 < 0 || s1 < s0) return jt::fail(JT_ERR_STATE, "invalid sample range");
+    if (s0 == s1) return JT_OK;
+    if (c->failed) return jt::fail(JT_ERR_STATE, "a previous launch failed; jt_reset the context");
+    if (c->first >= 0 && s0 != c->next)
+        return jt::fail(JT_ERR_STATE, "samples must be accumulated in order (expected " + std::to_string(c->next) + ")");
+    if (c->first < 0) c->first = s0;
+    if (!c->sub.empty()) return multi_trace_range(c, s0, s1);
+    int st = trace_launch(c, s0, s1, c->first);
+    if (st != JT_OK) return st;
+    float ms = 0;
+    st = trace_finish(c, &ms);
+    if (st != JT_OK) return st;
+    c->next = s1;
     return JT_OK;
 }
 
@@ -2715,6 +2909,7 @@ int jt_get_size(const jt_ctx* c, int32_t* w, int32_t* h) {
 int jt_get_image(jt_ctx* c, float* rgba) {
     if (!c || !rgba) return jt::fail(JT_ERR_INVALID, "NULL argument");
     if (c->failed) return jt::fail(JT_ERR_STATE, "the running means are corrupt (a launch failed); jt_reset the context");
+    if (!c->sub.empty()) return multi_reduce(c, 0, rgba, nullptr);
     (void)hipSetDevice(c->device);
     hipError_t e = hipMemcpy(rgba, c->A.image, (size_t)c->width * c->height * 16, hipMemcpyDeviceToHost);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy image");
@@ -2727,8 +2922,14 @@ int jt_get_aovs(jt_ctx* c, float* albedo, float* normal, int64_t* hits) {
     const size_t np = (size_t)c->width * c->height;
     std::vector<float4> tmp(np);
     hipError_t e;
+    const bool multi = !c->sub.empty();
+    int st;
     if (albedo) {
-        if ((e = hipMemcpy(tmp.data(), c->A.albedo, np * 16, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+        if (multi) {
+            if ((st = multi_reduce(c, 1, reinterpret_cast<float*>(tmp.data()), nullptr)) != JT_OK) return st;
+        } else if ((e = hipMemcpy(tmp.data(), c->A.albedo, np * 16, hipMemcpyDeviceToHost)) != hipSuccess) {
+            return hip_fail(e, "hipMemcpy");
+        }
         for (size_t k = 0; k < np; k++) {
             albedo[3 * k] = tmp[k].x;
             albedo[3 * k + 1] = tmp[k].y;
@@ -2736,7 +2937,11 @@ int jt_get_aovs(jt_ctx* c, float* albedo, float* normal, int64_t* hits) {
         }
     }
     if (normal) {
-        if ((e = hipMemcpy(tmp.data(), c->A.normal, np * 16, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+        if (multi) {
+            if ((st = multi_reduce(c, 2, reinterpret_cast<float*>(tmp.data()), nullptr)) != JT_OK) return st;
+        } else if ((e = hipMemcpy(tmp.data(), c->A.normal, np * 16, hipMemcpyDeviceToHost)) != hipSuccess) {
+            return hip_fail(e, "hipMemcpy");
+        }
         for (size_t k = 0; k < np; k++) {
             normal[3 * k] = tmp[k].x;
             normal[3 * k + 1] = tmp[k].y;
@@ -2744,13 +2949,36 @@ int jt_get_aovs(jt_ctx* c, float* albedo, float* normal, int64_t* hits) {
         }
     }
     if (hits) {
-        if ((e = hipMemcpy(hits, c->A.hits, np * 8, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
+        if (multi) {
+            if ((st = multi_reduce(c, 0, nullptr, hits)) != JT_OK) return st;
+        } else if ((e = hipMemcpy(hits, c->A.hits, np * 8, hipMemcpyDeviceToHost)) != hipSuccess) {
+            return hip_fail(e, "hipMemcpy");
+        }
     }
     return JT_OK;
 }
 
 int jt_get_counters(jt_ctx* c, jt_counters* out) {
     if (!c || !out) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    if (!c->sub.empty()) {  // summed over the devices; kernel_ms: per launch the slowest device
+        jt_counters sum{};
+        for (jt_ctx* s : c->sub) {
+            jt_counters k{};
+            const int st = jt_get_counters(s, &k);
+            if (st != JT_OK) return st;
+            sum.paths += k.paths;
+            sum.rays += k.rays;
+            sum.light_queries += k.light_queries;
+            sum.nodes += k.nodes;
+            sum.instances += k.instances;
+            sum.prims += k.prims;
+            sum.shades += k.shades;
+        }
+        sum.launches = c->launches;
+        sum.kernel_ms = c->kernel_ms;
+        *out = sum;
+        return JT_OK;
+    }
     (void)hipSetDevice(c->device);
     unsigned long long v[8] = {0};
     hipError_t e = hipMemcpy(v, c->A.counters, 7 * 8, hipMemcpyDeviceToHost);
@@ -2769,6 +2997,7 @@ int jt_get_counters(jt_ctx* c, jt_counters* out) {
 
 int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
     if (!c || !out) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    if (!c->sub.empty()) return jt_get_device_buffers(c->sub[0], out);  // device 0's share
     out->image = c->A.image;
     out->albedo = c->A.albedo;
     out->normal = c->A.normal;
@@ -2788,6 +3017,13 @@ extern "C" int jt_debug_stamps(jt_ctx* c, unsigned long long* out8) {
 
 int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     if (!c || !buf || n <= 0) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    if (!c->sub.empty()) {
+        char tmp[512];
+        const int st = jt_describe(c->sub[0], tmp, sizeof tmp);
+        if (st != JT_OK) return st;
+        std::snprintf(buf, (size_t)n, "%s devices=%d", tmp, (int)c->sub.size());
+        return JT_OK;
+    }
     const bool ovf = c->stack > 16;
     const int ring = ovf ? c->ring : 16;
     char tmp[512];
@@ -2804,12 +3040,18 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
 int jt_set_counters(jt_ctx* c, int32_t level) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
     if (level != 0 && level != 1) return jt::fail(JT_ERR_INVALID, "counter level must be 0 or 1");
+    for (jt_ctx* s : c->sub) s->count = level;
     c->count = level;
     return JT_OK;
 }
 
 int jt_synchronize(jt_ctx* c) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    for (jt_ctx* s : c->sub) {
+        const int st = jt_synchronize(s);
+        if (st != JT_OK) return st;
+    }
+    if (!c->sub.empty()) return JT_OK;
     (void)hipSetDevice(c->device);
     hipError_t e = hipStreamSynchronize(c->stream);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipStreamSynchronize");

@@ -258,6 +258,8 @@ def _declare(lib):
     lib.jt_image_size.argtypes = [C.POINTER(jt_scene), C.POINTER(jt_params), i32p, i32p]
     lib.jt_create.argtypes = [C.POINTER(jt_scene), C.POINTER(jt_scene_bvh), C.POINTER(jt_lights),
                               C.POINTER(jt_params), C.POINTER(C.c_void_p)]
+    lib.jt_create_multi.argtypes = [C.POINTER(jt_scene), C.POINTER(jt_scene_bvh), C.POINTER(jt_lights),
+                                    C.POINTER(jt_params), i32p, C.c_int32, C.POINTER(C.c_void_p)]
     lib.jt_trace_samples.argtypes = [C.c_void_p]
     lib.jt_trace_range.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
     lib.jt_get_samples.argtypes = [C.c_void_p, i32p]
@@ -278,7 +280,7 @@ def _declare(lib):
 # every symbol include/jtrace.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
     "jt_version", "jt_abi_version", "jt_last_error", "jt_device_count", "jt_build_scene_bvh",
-    "jt_free_scene_bvh", "jt_make_lights", "jt_free_lights", "jt_image_size", "jt_create",
+    "jt_free_scene_bvh", "jt_make_lights", "jt_free_lights", "jt_image_size", "jt_create", "jt_create_multi",
     "jt_trace_samples", "jt_trace_range", "jt_get_samples", "jt_get_size", "jt_get_image",
     "jt_get_aovs", "jt_get_counters", "jt_reset", "jt_get_device_buffers", "jt_set_counters", "jt_describe", "jt_synchronize",
     "jt_destroy",

@@ -2,7 +2,8 @@
 ArgParse table (:12-86), the SAMPLER_TYPES index (:88) and Params (:90-138).
 
 Extensions beyond the reference (all optional): --seed (RNG seed), --width/--height (explicit
-image size, camera aspect := W/H), --device, --missing (drop|error for incomplete scenes).
+image size, camera aspect := W/H), --device, --devices N (one context over GPUs 0..N-1:
+jt_create_multi), --missing (drop|error for incomplete scenes).
 """
 from __future__ import annotations
 
@@ -46,6 +47,8 @@ def _parser() -> argparse.ArgumentParser:
     p.add_argument("--width", type=int, default=0, help="image width (extension)")
     p.add_argument("--height", type=int, default=0, help="image height (extension)")
     p.add_argument("--device", type=int, default=0, help="HIP device (extension)")
+    p.add_argument("--devices", type=int, default=1,
+                   help="GPUs of this node to shard every batch over, devices 0..N-1 (extension)")
     p.add_argument("--missing", choices=["error", "drop"], default="error",
                    help="missing scene assets: error (reference) or drop (extension)")
     return p
@@ -75,6 +78,7 @@ class Params:
     width: int = 0
     height: int = 0
     device: int = 0
+    devices: int = 1
     missing: str = "error"
 
 

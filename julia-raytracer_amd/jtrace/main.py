@@ -59,7 +59,8 @@ def run(params: Params, out=print) -> dict:
     lights = make_trace_lights(scene_abi, lib)
     out("making state...")
     jp = abi.make_params(params, camera)
-    state = make_trace_state(scene_abi, bvh, lights, jp, lib)
+    devices = int(getattr(params, "devices", 1) or 1)
+    state = make_trace_state(scene_abi, bvh, lights, jp, lib, devices=list(range(devices)) if devices > 1 else None)
     out("tracing samples...")
     sampling_start = time.perf_counter()
     for _ in range(0, params.samples, params.batch):

@@ -86,12 +86,22 @@ def image_size(scene_abi, params: abi.jt_params, lib=None):
 class TraceState:
     """Device-resident TraceState (src/trace.jl:87-100): running-mean image/albedo/normal/hits."""
 
-    def __init__(self, scene_abi, bvh: SceneBvh, lights: TraceLights, params: abi.jt_params, lib=None):
+    def __init__(self, scene_abi, bvh: SceneBvh, lights: TraceLights, params: abi.jt_params, lib=None,
+                 devices=None):
+        """devices: None for one context on params.device (jt_create), or a list of HIP
+        ordinals for one context over those GPUs (jt_create_multi: every batch sharded across
+        them, the running means reduced with RCCL when read)."""
         self.lib = lib or abi.load_library()
         self._keep = (scene_abi, bvh, lights)
         self.params = params
         h = C.c_void_p()
-        abi.check(self.lib, self.lib.jt_create(scene_abi.ref, bvh.ref, lights.ref, C.byref(params), C.byref(h)))
+        if devices is None:
+            abi.check(self.lib, self.lib.jt_create(scene_abi.ref, bvh.ref, lights.ref, C.byref(params), C.byref(h)))
+        else:
+            devs = (C.c_int32 * len(devices))(*devices)
+            abi.check(self.lib, self.lib.jt_create_multi(scene_abi.ref, bvh.ref, lights.ref, C.byref(params), devs,
+                                                         len(devices), C.byref(h)))
+        self.devices = devices
         self.handle = h
         w, hh = C.c_int32(), C.c_int32()
         abi.check(self.lib, self.lib.jt_get_size(self.handle, C.byref(w), C.byref(hh)))
@@ -160,8 +170,8 @@ class TraceState:
         self.close()
 
 
-def make_trace_state(scene_abi, bvh, lights, params, lib=None) -> TraceState:
-    return TraceState(scene_abi, bvh, lights, params, lib)
+def make_trace_state(scene_abi, bvh, lights, params, lib=None, devices=None) -> TraceState:
+    return TraceState(scene_abi, bvh, lights, params, lib, devices)
 
 
 def trace_samples(state: TraceState):

@@ -172,16 +172,25 @@ mutable struct HipState
     height::Int
 end
 
-"""make_hip_state(scene, bvh, lights, params) — jt_create: uploads everything, zeroed
-accumulators (make_trace_state, src/trace.jl:189-213)."""
-function make_hip_state(scene::SceneData, bvh::SceneBvh, lights::TraceLights, params::Params; device = 0)
+"""make_hip_state(scene, bvh, lights, params; device = 0, devices = 1) — jt_create: uploads
+everything, zeroed accumulators (make_trace_state, src/trace.jl:189-213). devices > 1:
+jt_create_multi over GPUs 0 .. devices-1 — every trace_samples batch is sharded across them and
+get_image! returns their RCCL-reduced, sample-weighted running mean."""
+function make_hip_state(scene::SceneData, bvh::SceneBvh, lights::TraceLights, params::Params; device = 0,
+                        devices = 1)
     keep = Any[]
     cs = Ref(pack_scene(scene, keep)); cb = Ref(pack_bvh(bvh, keep)); cl = Ref(pack_lights(lights, keep))
     cp = Ref(pack_params(params; device = device))
     ctx = Ref{Ptr{Cvoid}}(C_NULL)
     GC.@preserve keep cs cb cl cp begin
-        check(ccall((:jt_create, LIB), Cint, (Ref{JtScene}, Ref{JtSceneBvh}, Ref{JtLights}, Ref{JtParams},
-                                              Ref{Ptr{Cvoid}}), cs, cb, cl, cp, ctx))
+        if devices > 1
+            check(ccall((:jt_create_multi, LIB), Cint, (Ref{JtScene}, Ref{JtSceneBvh}, Ref{JtLights}, Ref{JtParams},
+                                                        Ptr{Int32}, Int32, Ref{Ptr{Cvoid}}),
+                        cs, cb, cl, cp, C_NULL, Int32(devices), ctx))
+        else
+            check(ccall((:jt_create, LIB), Cint, (Ref{JtScene}, Ref{JtSceneBvh}, Ref{JtLights}, Ref{JtParams},
+                                                  Ref{Ptr{Cvoid}}), cs, cb, cl, cp, ctx))
+        end
     end
     w = Ref{Int32}(0); h = Ref{Int32}(0)
     check(ccall((:jt_get_size, LIB), Cint, (Ptr{Cvoid}, Ref{Int32}, Ref{Int32}), ctx[], w, h))
