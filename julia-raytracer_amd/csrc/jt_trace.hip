@@ -13,6 +13,7 @@
 // the traversal order (and hence hit tie-breaking) is exactly the reference's. The running
 // mean (lerp with w = 1/(s+1), src/trace.jl:631-648) is kept in registers across samples and
 // written once per launch.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -2035,8 +2036,42 @@ int hip_fail(hipError_t e, const char* what) {
     return jt::fail(JT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// RCCL, loaded on first use by a multi-device context (dlopen of the ROCm install's
+// librccl.so.1): single-device contexts never touch it, and a process that already loaded an
+// RCCL (e.g. torch's) shares that one instead of a second copy
+struct Rccl {
+    bool ok = false;
+    decltype(&ncclCommInitAll) CommInitAll;
+    decltype(&ncclCommDestroy) CommDestroy;
+    decltype(&ncclReduce) Reduce;
+    decltype(&ncclGroupStart) GroupStart;
+    decltype(&ncclGroupEnd) GroupEnd;
+    decltype(&ncclRedOpCreatePreMulSum) RedOpCreatePreMulSum;
+    decltype(&ncclRedOpDestroy) RedOpDestroy;
+    decltype(&ncclGetErrorString) GetErrorString;
+};
+const Rccl& rccl() {
+    static Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return x;
+        x.CommInitAll = (decltype(x.CommInitAll))dlsym(h, "ncclCommInitAll");
+        x.CommDestroy = (decltype(x.CommDestroy))dlsym(h, "ncclCommDestroy");
+        x.Reduce = (decltype(x.Reduce))dlsym(h, "ncclReduce");
+        x.GroupStart = (decltype(x.GroupStart))dlsym(h, "ncclGroupStart");
+        x.GroupEnd = (decltype(x.GroupEnd))dlsym(h, "ncclGroupEnd");
+        x.RedOpCreatePreMulSum = (decltype(x.RedOpCreatePreMulSum))dlsym(h, "ncclRedOpCreatePreMulSum");
+        x.RedOpDestroy = (decltype(x.RedOpDestroy))dlsym(h, "ncclRedOpDestroy");
+        x.GetErrorString = (decltype(x.GetErrorString))dlsym(h, "ncclGetErrorString");
+        x.ok = x.CommInitAll && x.CommDestroy && x.Reduce && x.GroupStart && x.GroupEnd && x.RedOpCreatePreMulSum &&
+               x.RedOpDestroy && x.GetErrorString;
+        return x;
+    }();
+    return r;
+}
 int nccl_fail(ncclResult_t r, const char* what) {
-    return jt::fail(JT_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+    return jt::fail(JT_ERR_DEVICE, std::string(what) + ": " + rccl().GetErrorString(r));
 }
 
 template <class T>
@@ -2139,7 +2174,7 @@ int jt_device_count(int32_t* out) {
 void jt_destroy(jt_ctx* c) {
     if (!c) return;
     if (!c->sub.empty() || !c->comms.empty()) {
-        for (ncclComm_t m : c->comms) (void)ncclCommDestroy(m);
+        for (ncclComm_t m : c->comms) (void)rccl().CommDestroy(m);
         if (!c->sub.empty()) {
             (void)hipSetDevice(c->sub[0]->device);
             if (c->red) (void)hipFree(c->red);
@@ -2750,6 +2785,7 @@ int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lig
         for (int k = 0; k < d; k++)
             if (devs[k] == devs[d]) return jt::fail(JT_ERR_INVALID, "a device is listed twice");
     }
+    if (!rccl().ok) return jt::fail(JT_ERR_UNSUPPORTED, "librccl.so.1 (RCCL) could not be loaded");
     jt_ctx* c = new jt_ctx();
     for (int d = 0; d < ndevices; d++) {
         jt_params p = *params;
@@ -2764,7 +2800,7 @@ int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lig
     }
     c->nsub.assign(ndevices, 0);
     c->comms.resize(ndevices);
-    ncclResult_t r = ncclCommInitAll(c->comms.data(), ndevices, devs.data());
+    ncclResult_t r = rccl().CommInitAll(c->comms.data(), ndevices, devs.data());
     if (r != ncclSuccess) {
         c->comms.clear();
         jt_destroy(c);
@@ -2909,34 +2945,34 @@ int multi_reduce(jt_ctx* c, int which, float* out4, int64_t* hits) {
     if (out4) {
         for (int d = 0; d < D; d++) {
             w[d] = N > 0 ? (float)((double)c->nsub[d] / (double)N) : (d == 0 ? 1.0f : 0.0f);
-            if ((r = ncclRedOpCreatePreMulSum(&ops[d], &w[d], ncclFloat32, ncclScalarHostImmediate, c->comms[d])) != ncclSuccess)
+            if ((r = rccl().RedOpCreatePreMulSum(&ops[d], &w[d], ncclFloat32, ncclScalarHostImmediate, c->comms[d])) != ncclSuccess)
                 return nccl_fail(r, "ncclRedOpCreatePreMulSum");
         }
     }
-    if ((r = ncclGroupStart()) != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
+    if ((r = rccl().GroupStart()) != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
     for (int d = 0; d < D; d++) {
         jt_ctx* s = c->sub[d];
         (void)hipSetDevice(s->device);
         if (out4) {
             const float4* src = which == 0 ? s->A.image : which == 1 ? s->A.albedo : s->A.normal;
-            r = ncclReduce(src, d == 0 ? (void*)c->red : (void*)src, np * 4, ncclFloat32, ops[d], 0, c->comms[d], s->stream);
+            r = rccl().Reduce(src, d == 0 ? (void*)c->red : (void*)src, np * 4, ncclFloat32, ops[d], 0, c->comms[d], s->stream);
         } else {
-            r = ncclReduce(s->A.hits, d == 0 ? (void*)c->red_hits : (void*)s->A.hits, np, ncclInt64, ncclSum, 0, c->comms[d],
+            r = rccl().Reduce(s->A.hits, d == 0 ? (void*)c->red_hits : (void*)s->A.hits, np, ncclInt64, ncclSum, 0, c->comms[d],
                            s->stream);
         }
         if (r != ncclSuccess) {
-            (void)ncclGroupEnd();
+            (void)rccl().GroupEnd();
             return nccl_fail(r, "ncclReduce");
         }
     }
-    if ((r = ncclGroupEnd()) != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
+    if ((r = rccl().GroupEnd()) != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
     hipError_t e;
     for (int d = 0; d < D; d++) {
         (void)hipSetDevice(c->sub[d]->device);
         if ((e = hipStreamSynchronize(c->sub[d]->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     }
     if (out4)
-        for (int d = 0; d < D; d++) (void)ncclRedOpDestroy(ops[d], c->comms[d]);
+        for (int d = 0; d < D; d++) (void)rccl().RedOpDestroy(ops[d], c->comms[d]);
     (void)hipSetDevice(c->sub[0]->device);
     if (out4) e = hipMemcpy(out4, c->red, np * 16, hipMemcpyDeviceToHost);
     else e = hipMemcpy(hits, c->red_hits, np * 8, hipMemcpyDeviceToHost);
