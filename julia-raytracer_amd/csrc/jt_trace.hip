@@ -23,7 +23,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
-#include <type_traits>
 #include <vector>
 
 #include "jt_bsdf.h"
@@ -693,12 +692,6 @@ __host__ __device__ constexpr bool lane_lds(int F) { return JT_LANE_LDS && F != 
 // HBM-mode kernels (GAOV): the albedo / normal running means are read-modified-written in HBM
 // (L2) instead of LDS slots 4..9, which their 64-bit traversal stacks need (4 workgroups per CU);
 // the remaining slots move down: 4 hits, 5 sample, 6 weight.
-#ifndef JT_GAOV
-#define JT_GAOV 1
-#endif
-#ifndef JT_WIDE_STACK
-#define JT_WIDE_STACK 1
-#endif
 __host__ __device__ constexpr int acc_hits(bool gaov) { return gaov ? 4 : 10; }
 __host__ __device__ constexpr int acc_slots(bool ll, bool gaov) { return acc_hits(gaov) + (ll ? 3 : 1); }
 constexpr int ACC_SLOTS = JT_LANE_LDS ? 13 : 11;  // LDS mode's larger layout (the host sizes LDS with it)
@@ -998,7 +991,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     constexpr bool LL = lane_lds(F);
-    constexpr bool GAOV = NCACHE && JT_GAOV;  // HBM mode: albedo / normal means in HBM (Aov)
+    constexpr bool GAOV = NCACHE;  // HBM mode: albedo / normal means in HBM (Aov)
     constexpr int HS = acc_hits(GAOV);  // LDS slots: 0..3 image, [4..9 albedo / normal,] HS hits, HS+1 sample, HS+2 weight
     __shared__ float acc_lds[acc_slots(LL, GAOV) * BLOCK];
     float* acc = acc_lds + threadIdx.x;
@@ -1857,8 +1850,7 @@ __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob)
 // the measured limiter of this mode).
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
-    using SE = std::conditional_t<JT_WIDE_STACK != 0, uint2, unsigned>;
-    __shared__ SE lds_stack[RING * BLOCK];  // 64-bit entries: {info, t0} (node_step)
+    __shared__ uint2 lds_stack[RING * BLOCK];  // 64-bit entries: {info, t0} (node_step)
     extern __shared__ uint4 node_cache[];
     const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
     for (int k = threadIdx.x; k < 2 * S.nlnodes; k += BLOCK) node_cache[k] = src[k];
@@ -2640,8 +2632,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         // overflow, just the scene's bound
         const size_t acc_bytes = (size_t)ACC_SLOTS * BLOCK * 4;
         // HBM mode: 64-bit stack entries, albedo / normal means in HBM (acc_slots(.., true))
-        const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * (JT_WIDE_STACK ? 8 : 4) +
-                                  (size_t)acc_slots(true, JT_GAOV != 0) * BLOCK * 4;
+        const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 8 + (size_t)acc_slots(true, true) * BLOCK * 4;
         const size_t lds_base = (size_t)(c->stack <= 16 ? c->stack : c->ring) * BLOCK * 4 + acc_bytes;
         const size_t bytes = blob.size() * 16;
         const size_t lds_cu = 160 * 1024;
