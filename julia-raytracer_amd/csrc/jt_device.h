@@ -128,7 +128,7 @@ struct DScene {
     const DNode* lnodes;
     int nlnodes;
     // traversal-stack overflow (scenes deeper than the LDS ring): ovf_stride entries per pixel
-    void* ovf;  // 32-bit (LDS mode) or 64-bit (HBM mode) entries: the kernel's stack entry type
+    int* ovf;
     int ovf_stride;
     int ring;  // entries of the LDS ring in use (a power of two <= the kernel's RING)
     int stack_need;  // stack bound of the scene: LDS-mode kernels without overflow allocate this many
@@ -514,21 +514,6 @@ __device__ __forceinline__ bool intersect_bbox(v3 o, v3 dinv, float tmin, float 
                __builtin_isnan(My) | __builtin_isnan(Mz);
     float t0 = vmax3(vmin(mx, Mx), vmin(my, My), vmax(vmin(mz, Mz), tmin));
     float t1 = vmin3(vmax(mx, Mx), vmax(my, My), vmin(vmax(mz, Mz), tmax));
-    return !nan && ((double)t0 <= (double)t1 * 1.00000024);
-}
-
-// intersect_bbox that also returns t0, the slab test's entry distance max(slab minima, tmin):
-// independent of tmax, it lets a pre-tested child's later test be one compare (node_step)
-__device__ __forceinline__ bool intersect_bbox_t0(v3 o, v3 dinv, float tmin, float tmax, const float4& a,
-                                                  const float4& b, float& t0out) {
-    const float mx = (a.x - o.x) * dinv.x, Mx = (a.y - o.x) * dinv.x;
-    const float my = (a.z - o.y) * dinv.y, My = (a.w - o.y) * dinv.y;
-    const float mz = (b.x - o.z) * dinv.z, Mz = (b.y - o.z) * dinv.z;
-    bool nan = __builtin_isnan(mx) | __builtin_isnan(my) | __builtin_isnan(mz) | __builtin_isnan(Mx) |
-               __builtin_isnan(My) | __builtin_isnan(Mz);
-    float t0 = vmax3(vmin(mx, Mx), vmin(my, My), vmax(vmin(mz, Mz), tmin));
-    float t1 = vmin3(vmax(mx, Mx), vmax(my, My), vmin(vmax(mz, Mz), tmax));
-    t0out = t0;
     return !nan && ((double)t0 <= (double)t1 * 1.00000024);
 }
 

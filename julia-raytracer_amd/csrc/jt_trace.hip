@@ -253,15 +253,16 @@ __device__ __forceinline__ v3 eval_environment(const DScene& S, v3 direction) {
 }
 
 // ============================================================================ traversal (src/bvh.jl)
-// Unified per-lane stack in LDS (entry formats: StackEnt below; jt_create checks the scene's
-// indices fit). Layout stack[k * BLOCK + lane]: every lane owns its bank(s), conflict-free
-// whatever the per-lane depth.
+// Unified per-lane stack in LDS, entry = type << 30 | snap << 24 | index (24 bits; jt_create
+// checks the scene fits). snap (HBM mode): the query's hit count when a pre-tested child was
+// pushed (SNAP_NONE: not pre-tested). Layout stack[k * BLOCK + lane]:
+// every lane owns one bank (conflict-free ds_read/write_b32 whatever the per-lane depth).
 // The LDS part is a ring of RING entries; when a scene's bound exceeds it (OVF), the oldest
 // entries spill to a per-pixel HBM area and come back one at a time when popped.
 constexpr int BLOCK = 256;
 constexpr unsigned T_TLAS = 0u, T_INST = 1u, T_BLAS = 2u;
 constexpr unsigned IDX_MASK = (1u << 24) - 1;
-constexpr unsigned SNAP_NONE = 0u;  // (round 1's hit-count snapshot bits; superseded by t0 entries)
+constexpr unsigned SNAP_NONE = 63u << 24;
 
 struct Hit {
     int inst, elem;
@@ -292,6 +293,7 @@ struct Trav {
     int prim, nprim;   // leaf cursor: next primitive record, primitives left
     int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
     float h_u, h_v;
+    int nh;              // hits accepted so far (every tmax change), saturating at 63
 };
 
 __device__ __forceinline__ int neg_mask(v3 d) { return (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0); }
@@ -310,35 +312,7 @@ __device__ __forceinline__ Hit query_hit(const Trav& T) {
 
 __device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T.nprim > 0; }
 
-// Stack entries. LDS-mode kernels: 32 bits, type << 30 | index (24 bits). HBM-mode kernels
-// (NCACHE): 64 bits, {info, t0}: either the same 32-bit form (t0 unused) or, for a child box
-// tested at its parent (the child pre-test, node_step), PRE | its node's internal / axis / num /
-// start packed in info and its slab-test entry distance t0: the pop-time box test is then the
-// exact compare t0 <= tmax * (1 + eps) (see node_step) and needs no load of the node at all.
-template <class SE>
-struct StackEnt;
-template <>
-struct StackEnt<unsigned> {
-    static __device__ __forceinline__ unsigned make(unsigned info, float) { return info; }
-    static __device__ __forceinline__ unsigned info(unsigned e) { return e; }
-    static __device__ __forceinline__ float t0(unsigned) { return 0.0f; }
-};
-template <>
-struct StackEnt<uint2> {
-    static __device__ __forceinline__ uint2 make(unsigned info, float t0) { return make_uint2(info, __float_as_uint(t0)); }
-    static __device__ __forceinline__ unsigned info(uint2 e) { return e.x; }
-    static __device__ __forceinline__ float t0(uint2 e) { return __uint_as_float(e.y); }
-};
-// pre-tested child entry (64-bit stacks): type | PRE | internal | axis | num | start (23 bits)
-constexpr unsigned PRE_BIT = 1u << 29, PRE_INTERNAL = 1u << 28, START_MASK = (1u << 23) - 1;
-__device__ __forceinline__ unsigned pre_info(unsigned type, float start_bits, float meta_bits) {
-    const unsigned meta = __float_as_uint(meta_bits);
-    const unsigned internal = meta >> 24, axis = (meta >> 16) & 3u, num = meta & 7u;
-    return type << 30 | PRE_BIT | internal << 28 | axis << 26 | num << 23 | (__float_as_uint(start_bits) & START_MASK);
-}
-
-template <class SE>
-__device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, SE* stack) {
+__device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, int* stack) {
     T.wo = o;
     T.wd = d;
     T.wdinv = V3(jl_rcp(d.x), jl_rcp(d.y), jl_rcp(d.z));  // ray_dinv (src/bvh.jl:322), no guard
@@ -346,6 +320,7 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     T.ld = d;
     T.ldinv = T.wdinv;
     T.tmax = __builtin_inff();
+    T.nh = 0;
     T.h_inst = -1;
     T.h_elem = -1;
     T.h_u = 0;
@@ -356,7 +331,7 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     T.cur_kind = KIND_TRI;
     T.inst_space = 0;
     T.negmask = neg_mask(d);
-    stack[0] = StackEnt<SE>::make(root, 0.0f);
+    stack[0] = (int)root;
     T.sp = 1;
     T.low = 0;
 }
@@ -377,6 +352,7 @@ __device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
     const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.y, r0.w, r1.y), V3(r1.w, r2.y, r2.w),
                                               V3(r3.y, r3.w, r4.y));
     if (tri_hit_before(p1, T.tmax)) {
+        T.nh += T.nh < 63 ? 1 : 0;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.z);
         T.h_u = p1.u;
@@ -384,6 +360,7 @@ __device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
         T.tmax = p1.t;
     }
     if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax)) {
+        T.nh += T.nh < 63 ? 1 : 0;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.w);
         T.h_u = p2.u;
@@ -410,6 +387,7 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     const float4 a = r[0], b = r[1], c = r[2], d = r[3];
     const PrimHit p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
     if (p.hit) {
+        T.nh += T.nh < 63 ? 1 : 0;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(a.w);
         T.h_u = p.u;
@@ -420,122 +398,108 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     T.nprim -= 1;
 }
 
-template <int RING, bool OVF, class SE>
-__device__ __forceinline__ void st_push(const DScene& S, Trav& T, SE* stack, int pixel, SE e) {
+template <int RING, bool OVF>
+__device__ __forceinline__ void st_push(const DScene& S, Trav& T, int* stack, int pixel, unsigned e) {
     if (OVF) {
-        SE* const ovf = reinterpret_cast<SE*>(S.ovf);
         if (T.sp - T.low == S.ring) {  // ring full: the oldest entry moves to HBM
-            ovf[(size_t)pixel * S.ovf_stride + T.low] = stack[(T.low & (S.ring - 1)) * BLOCK];
+            S.ovf[(size_t)pixel * S.ovf_stride + T.low] = stack[(T.low & (S.ring - 1)) * BLOCK];
             T.low += 1;
         }
-        stack[(T.sp & (S.ring - 1)) * BLOCK] = e;
+        stack[(T.sp & (S.ring - 1)) * BLOCK] = (int)e;
     } else {
-        stack[T.sp * BLOCK] = e;
+        stack[T.sp * BLOCK] = (int)e;
     }
     T.sp += 1;
 }
-template <int RING, bool OVF, class SE>
-__device__ __forceinline__ SE st_pop(const DScene& S, Trav& T, const SE* stack, int pixel) {
+template <int RING, bool OVF>
+__device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* stack, int pixel) {
     T.sp -= 1;
     if (OVF) {
         if (T.sp < T.low) {  // below the ring: this entry was spilled
             T.low = T.sp;
-            return reinterpret_cast<const SE*>(S.ovf)[(size_t)pixel * S.ovf_stride + T.sp];
+            return (unsigned)S.ovf[(size_t)pixel * S.ovf_stride + T.sp];
         }
-        return stack[(T.sp & (S.ring - 1)) * BLOCK];
+        return (unsigned)stack[(T.sp & (S.ring - 1)) * BLOCK];
     }
-    return stack[T.sp * BLOCK];
+    return (unsigned)stack[T.sp * BLOCK];
 }
 
 // Pop one stack entry: an instance entry or a TLAS/BLAS node. An instance visit and the box
 // test of its BLAS root are one step: the reference's instance visit pushes nothing but the
 // root (src/bvh.jl:345-351, 502-506), which is then the very next pop, so testing it in the same
 // step visits the same nodes in the same order.
-//
-// 64-bit stacks (HBM mode): when an internal node passes, both children (one adjacent 64-B pair)
-// are tested at once with the current tmax, and only the survivors are pushed, each with its
-// slab-test entry distance t0 and its start / meta. Exact, per intersect_bbox
-// (src/geometry.jl:96-105): t0 = max(slab minima, tmin) does not depend on tmax, and
-// t1 = min(M, tmax) with M the slab maxima's minimum. A child that fails now fails when the
-// reference pops it too (tmax only shrinks; the test is monotone in it): its pop is counted, its
-// push skipped. A survivor satisfied t0 <= min(M, tmax_push) * c (in double, c = 1.00000024), so
-// at its pop, with tmax <= tmax_push, the reference's test t0 <= min(M, tmax) * c is exactly
-// t0 <= tmax * c: if tmax < M both are that, else both hold (t0 <= M * c <= tmax * c, rounding
-// being monotone). The pop then loads nothing: one compare, and the start / meta it carries.
-template <int RING, bool OVF, int COUNT, bool NCACHE, int F, class SE>
-__device__ __forceinline__ void node_step(const DScene& S, Trav& T, SE* stack, int pixel, Counters& cnt) {
+template <int RING, bool OVF, int COUNT, bool NCACHE, int F>
+__device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
     // without FT_XFORM every instance ray is the world ray: no transform, no space switch
     constexpr bool XF = (F & FT_XFORM) != 0;
-    constexpr bool WIDE = sizeof(SE) == 8;
-    const SE e = st_pop<RING, OVF>(S, T, stack, pixel);
-    const unsigned info = StackEnt<SE>::info(e);
-    unsigned type = info >> 30;
-    bool internal;
-    int start, num, axis;
-    if (WIDE && (info & PRE_BIT)) {
-        // a pre-tested child: its box test is t0 against the current tmax (above)
-        if (COUNT) cnt.nodes++;
-        if (!((double)StackEnt<SE>::t0(e) <= (double)T.tmax * 1.00000024)) return;
-        if (XF && type == T_TLAS && T.inst_space) world_ray(T);  // back from an instance
-        internal = (info & PRE_INTERNAL) != 0;
-        axis = (int)((info >> 26) & 3u);
-        num = (int)((info >> 23) & 7u);
-        start = (int)(info & START_MASK);
-    } else {
-        unsigned idx = info & IDX_MASK;
-        if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
-            if (COUNT) cnt.instances++;
-            const int4 ib = S.inst_blas[idx];  // blas_root, kind, identity, shape
-            if (!XF || ib.z) {
-                // inverse(identity) is exactly the identity: transform_ray returns the ray bit for bit
-                if (XF && T.inst_space) world_ray(T);
-            } else {
-                const DInstTrav it = S.inst_trav[idx];
-                const fr3 inv = frame_from(it.i0, it.i1, it.i2);
-                T.lo = transform_point(inv, T.wo);
-                T.ld = transform_vector(inv, T.wd);
-                T.ldinv = V3(jl_rcp(T.ld.x), jl_rcp(T.ld.y), jl_rcp(T.ld.z));
-                T.negmask = neg_mask(T.ld);
-                T.inst_space = 1;
-            }
-            T.cur_inst = (int)idx;
-            T.cur_kind = ib.y;
-            type = T_BLAS;
-            idx = (unsigned)ib.x;
-        } else if (XF && type == T_TLAS && T.inst_space) {
-            world_ray(T);  // back from an instance: TLAS nodes test the world ray
+    const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
+    unsigned type = e >> 30, idx = e & IDX_MASK;
+    if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
+        if (COUNT) cnt.instances++;
+        const int4 ib = S.inst_blas[idx];  // blas_root, kind, identity, shape
+        if (!XF || ib.z) {
+            // inverse(identity) is exactly the identity: transform_ray returns the ray bit for bit
+            if (XF && T.inst_space) world_ray(T);
+        } else {
+            const DInstTrav it = S.inst_trav[idx];
+            const fr3 inv = frame_from(it.i0, it.i1, it.i2);
+            T.lo = transform_point(inv, T.wo);
+            T.ld = transform_vector(inv, T.wd);
+            T.ldinv = V3(jl_rcp(T.ld.x), jl_rcp(T.ld.y), jl_rcp(T.ld.z));
+            T.negmask = neg_mask(T.ld);
+            T.inst_space = 1;
         }
-        if (COUNT) cnt.nodes++;
-        const DNode nd = (NCACHE && (int)idx < S.nlnodes) ? S.lnodes[idx] : S.nodes[idx];
-        if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
-        const unsigned meta = __float_as_uint(nd.b.w);
-        start = __float_as_int(nd.b.z);
-        num = (int)(meta & 0xffffu);
-        axis = (int)((meta >> 16) & 0xffu);
-        internal = (meta >> 24) != 0;
+        T.cur_inst = (int)idx;
+        T.cur_kind = ib.y;
+        type = T_BLAS;
+        idx = (unsigned)ib.x;
+    } else if (XF && type == T_TLAS && T.inst_space) {
+        world_ray(T);  // back from an instance: TLAS nodes test the world ray
     }
     const bool blas = type == T_BLAS;
-    if (internal) {  // for d[axis] >= 0 push start, start+1 (start+1 pops first)
+    if (COUNT) cnt.nodes++;
+    // HBM mode: a child pre-tested at its parent with the tmax it still has (no hit since: its
+    // snapshot equals the hit count) passes this pop's box test too — same ray, same box, same
+    // tmax — so only its start/meta half is loaded
+    const unsigned snap = (e >> 24) & 63u;
+    float4 nb;
+    if (NCACHE && snap != 63u && snap == (unsigned)T.nh) {
+        nb = ((int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
+    } else {
+        const DNode nd = (NCACHE && (int)idx < S.nlnodes) ? S.lnodes[idx] : S.nodes[idx];
+        if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
+        nb = nd.b;
+    }
+    const unsigned meta = __float_as_uint(nb.w);
+    const int start = __float_as_int(nb.z);
+    const int num = (int)(meta & 0xffffu);
+    if (meta >> 24) {  // internal: for d[axis] >= 0 push start, start+1 (start+1 pops first)
+        const int axis = (int)((meta >> 16) & 0xffu);
         const bool neg = (T.negmask >> axis) & 1;  // d[axis] < 0
+        const unsigned tag = type << 30 | SNAP_NONE;
         const unsigned c_far = (unsigned)(neg ? start + 1 : start), c_near = (unsigned)(neg ? start : start + 1);
-        if (WIDE && JT_CHILD_PRETEST) {
-            const bool cached = NCACHE && (int)c_near < S.nlnodes && (int)c_far < S.nlnodes;
+        if (JT_CHILD_PRETEST && NCACHE) {
+            // HBM mode: test both children (one 64-B pair) when their parent is visited. A child
+            // whose box fails now fails when popped too (the slab test is monotone in tmax, which
+            // only shrinks): count its pop and skip the push. A pushed child is tested again when
+            // popped, with that moment's tmax, exactly as the reference does. (+10 % bathroom1,
+            // +14 % ecosys; in LDS mode the extra tests cost more than the pops they save.)
+            const bool cached = (int)c_near < S.nlnodes && (int)c_far < S.nlnodes;
             const DNode n0 = cached ? S.lnodes[c_far] : S.nodes[c_far];
             const DNode n1 = cached ? S.lnodes[c_near] : S.nodes[c_near];
-            float t00, t01;
-            const bool k0 = intersect_bbox_t0(T.lo, T.ldinv, ray_eps, T.tmax, n0.a, n0.b, t00);
-            const bool k1 = intersect_bbox_t0(T.lo, T.ldinv, ray_eps, T.tmax, n1.a, n1.b, t01);
+            const bool k0 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n0.a, n0.b);
+            const bool k1 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n1.a, n1.b);
             if (COUNT) cnt.nodes += (k0 ? 0 : 1) + (k1 ? 0 : 1);
-            if (k0) st_push<RING, OVF>(S, T, stack, pixel, StackEnt<SE>::make(pre_info(type, n0.b.z, n0.b.w), t00));
-            if (k1) st_push<RING, OVF>(S, T, stack, pixel, StackEnt<SE>::make(pre_info(type, n1.b.z, n1.b.w), t01));
+            const unsigned ptag = type << 30 | (unsigned)T.nh << 24;  // pre-tested at hit count nh
+            if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_far);
+            if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_near);
         } else {
-            const unsigned tag = type << 30;
-            st_push<RING, OVF>(S, T, stack, pixel, StackEnt<SE>::make(tag | c_far, 0.0f));
-            st_push<RING, OVF>(S, T, stack, pixel, StackEnt<SE>::make(tag | c_near, 0.0f));
+            st_push<RING, OVF>(S, T, stack, pixel, tag | c_far);
+            st_push<RING, OVF>(S, T, stack, pixel, tag | c_near);
         }
     } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
         for (int k = num - 1; k >= 0; k--)
-            st_push<RING, OVF>(S, T, stack, pixel, StackEnt<SE>::make((T_INST << 30) | (unsigned)S.tlas_prims[start + k], 0.0f));
+            st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | SNAP_NONE | (unsigned)S.tlas_prims[start + k]);
     } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
@@ -689,24 +653,15 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
 // Not in the FT_NONE kernels: cornellbox's LDS-mode kernel then no longer fits 5 workgroups per
 // CU (-9 %); the mesh kernels gain (features2 +7 %, bathroom1 +1 %, ecosys +0.6 %).
 __host__ __device__ constexpr bool lane_lds(int F) { return JT_LANE_LDS && F != FT_NONE; }
-// HBM-mode kernels (GAOV): the albedo / normal running means are read-modified-written in HBM
-// (L2) instead of LDS slots 4..9, which their 64-bit traversal stacks need (4 workgroups per CU);
-// the remaining slots move down: 4 hits, 5 sample, 6 weight.
-__host__ __device__ constexpr int acc_hits(bool gaov) { return gaov ? 4 : 10; }
-__host__ __device__ constexpr int acc_slots(bool ll, bool gaov) { return acc_hits(gaov) + (ll ? 3 : 1); }
-constexpr int ACC_SLOTS = JT_LANE_LDS ? 13 : 11;  // LDS mode's larger layout (the host sizes LDS with it)
-template <bool GAOV>
+constexpr int ACC_SLOTS = JT_LANE_LDS ? 13 : 11;  // the host sizes LDS for the larger layout
 struct Aov {
     float* acc;
     float w_;  // !lane_lds(F)
-    float4* albedo;  // GAOV: the HBM running means, and the lane's pixel from its 8x8 tile
-    float4* normal;
-    int tile_pixel0, width;
     template <int F>
-    __device__ __forceinline__ float w() const { return lane_lds(F) ? acc[(acc_hits(GAOV) + 2) * BLOCK] : w_; }
+    __device__ __forceinline__ float w() const { return lane_lds(F) ? acc[12 * BLOCK] : w_; }
 };
 template <int F>
-__device__ __forceinline__ void aov_update(const Aov<false>& a, v3 ta, v3 tn) {
+__device__ __forceinline__ void aov_update(const Aov& a, v3 ta, v3 tn) {
     const float aw = a.w<F>();
     const float omw = 1 - aw;
     float* p = a.acc;
@@ -716,23 +671,6 @@ __device__ __forceinline__ void aov_update(const Aov<false>& a, v3 ta, v3 tn) {
     p[7 * BLOCK] = p[7 * BLOCK] * omw + tn.x * aw;
     p[8 * BLOCK] = p[8 * BLOCK] * omw + tn.y * aw;
     p[9 * BLOCK] = p[9 * BLOCK] * omw + tn.z * aw;
-}
-__device__ __forceinline__ int opaque_lane_id();
-template <int F>
-__device__ __forceinline__ void aov_update(const Aov<true>& a, v3 ta, v3 tn) {
-    const float aw = a.w<F>();
-    const float omw = 1 - aw;
-    const int lx = opaque_lane_id();
-    const int pixel = a.tile_pixel0 + (lx >> 3) * a.width + (lx & 7);
-    float4 al = a.albedo[pixel], nr = a.normal[pixel];
-    al.x = al.x * omw + ta.x * aw;
-    al.y = al.y * omw + ta.y * aw;
-    al.z = al.z * omw + ta.z * aw;
-    nr.x = nr.x * omw + tn.x * aw;
-    nr.y = nr.y * omw + tn.y * aw;
-    nr.z = nr.z * omw + tn.z * aw;
-    a.albedo[pixel] = al;
-    a.normal[pixel] = nr;
 }
 
 template <int F, class AovT>
@@ -985,15 +923,13 @@ __device__ __forceinline__ int opaque_lane_id() {
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
 // mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, class SE>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
-                                           SE* stack) {
+                                           int* stack) {
     const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     constexpr bool LL = lane_lds(F);
-    constexpr bool GAOV = NCACHE;  // HBM mode: albedo / normal means in HBM (Aov)
-    constexpr int HS = acc_hits(GAOV);  // LDS slots: 0..3 image, [4..9 albedo / normal,] HS hits, HS+1 sample, HS+2 weight
-    __shared__ float acc_lds[acc_slots(LL, GAOV) * BLOCK];
+    __shared__ float acc_lds[(LL ? 13 : 11) * BLOCK];
     float* acc = acc_lds + threadIdx.x;
 #if JT_STAMPS
     unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
@@ -1024,28 +960,25 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     bool alive = in_image;
     int sample = cs0;
     if (in_image) {
-        const float4 im = A.image[pixel];
+        const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
         acc[0] = im.x;
         acc[BLOCK] = im.y;
         acc[2 * BLOCK] = im.z;
         acc[3 * BLOCK] = im.w;
-        if (!GAOV) {
-            const float4 al = A.albedo[pixel], nr = A.normal[pixel];
-            acc[4 * BLOCK] = al.x;
-            acc[5 * BLOCK] = al.y;
-            acc[6 * BLOCK] = al.z;
-            acc[7 * BLOCK] = nr.x;
-            acc[8 * BLOCK] = nr.y;
-            acc[9 * BLOCK] = nr.z;
-        }
-        reinterpret_cast<int*>(acc)[HS * BLOCK] = 0;
+        acc[4 * BLOCK] = al.x;
+        acc[5 * BLOCK] = al.y;
+        acc[6 * BLOCK] = al.z;
+        acc[7 * BLOCK] = nr.x;
+        acc[8 * BLOCK] = nr.y;
+        acc[9 * BLOCK] = nr.z;
+        reinterpret_cast<int*>(acc)[10 * BLOCK] = 0;
     }
     int* const acc_i = reinterpret_cast<int*>(acc);
-    Aov<GAOV> aov{acc, 0.0f, A.albedo, A.normal, (ut / tiles_x) * 8 * P.width + (ut % tiles_x) * 8, P.width};
+    Aov aov{acc, 0.0f};
     if (LL) {
         if (in_image) {
-            acc_i[(HS + 1) * BLOCK] = sample;
-            acc[(HS + 2) * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+            acc_i[11 * BLOCK] = sample;
+            acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
         }
     } else {
         aov.w_ = 1.0f / (float)(sample - P.first + 1);
@@ -1153,7 +1086,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 if (!all_finite(radiance)) radiance = V3(0, 0, 0);
                 const float mr = max3(radiance);
                 if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
-                const float w = aov.template w<F>();
+                const float w = aov.w<F>();
                 const float omw = 1 - w;
                 const bool hit = st.flags & F_HIT;
                 const bool env = !hit && !P.envhidden && S.nenvs != 0;
@@ -1164,17 +1097,17 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 acc[BLOCK] = acc[BLOCK] * omw + target.y * w;
                 acc[2 * BLOCK] = acc[2 * BLOCK] * omw + target.z * w;
                 acc[3 * BLOCK] = acc[3 * BLOCK] * omw + target.w * w;
-                if (hit || env) reinterpret_cast<int*>(acc)[HS * BLOCK] += 1;
+                if (hit || env) reinterpret_cast<int*>(acc)[10 * BLOCK] += 1;
                 if constexpr (LL) {
                 // the pixel from the unit's wave-uniform tile and a lane id the compiler cannot
                 // reuse from the top of the unit, so i / j do not stay live across the loop
-                const int sample = acc_i[(HS + 1) * BLOCK] + 1;
+                const int sample = acc_i[11 * BLOCK] + 1;
                 if (sample >= cs1) {
                     alive = false;
                     T.sp = -1;
                 } else {
-                    acc_i[(HS + 1) * BLOCK] = sample;
-                    acc[(HS + 2) * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+                    acc_i[11 * BLOCK] = sample;
+                    acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
                     const int lx = opaque_lane_id();
                     const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
                     start_path(P, i2, j2, j2 * P.width + i2, sample, st);
@@ -1224,11 +1157,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     }
     if (in_image) {
         A.image[pixel] = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);
-        if (!GAOV) {
-            A.albedo[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
-            A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
-        }
-        A.hits[pixel] += reinterpret_cast<const int*>(acc)[HS * BLOCK];
+        A.albedo[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
+        A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
+        A.hits[pixel] += reinterpret_cast<const int*>(acc)[10 * BLOCK];
     }
     if (uc + 1 < nchunks) publish_tile(A, ut, uc);
     }  // units
@@ -1438,7 +1369,7 @@ __device__ __forceinline__ void wf_push(WfCtl& C, int* ring, int NP, int q, bool
 #endif
 
 template <int SAMPLER, int COUNT, int F, bool NCACHE>
-__device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A, unsigned* stack,
+__device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A, int* stack,
                               int* lds_wf, float4* pool) {
     constexpr int RQ = wf_rec_q(F);
     const int lane = threadIdx.x & 63;
@@ -1850,7 +1781,7 @@ __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob)
 // the measured limiter of this mode).
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
-    __shared__ uint2 lds_stack[RING * BLOCK];  // 64-bit entries: {info, t0} (node_step)
+    __shared__ int lds_stack[RING * BLOCK];
     extern __shared__ uint4 node_cache[];
     const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
     for (int k = threadIdx.x; k < 2 * S.nlnodes; k += BLOCK) node_cache[k] = src[k];
@@ -1870,7 +1801,7 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(D
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
     const DScene L = blob_scene(S, blob);
-    trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<unsigned*>(dyn_lds) + threadIdx.x);
+    trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
 }
 
 // WF kernels (trace_body_wf, stack bound <= 16): dynamic LDS = the lanes' stacks, the WF rings /
@@ -1880,8 +1811,8 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_WF void trace_kernel_wf(DSce
                                                                             DAccum A, float4* pool) {
     extern __shared__ uint4 dyn_lds[];
     const int NP = 64 * P.wf_groups;
-    unsigned* const stack = reinterpret_cast<unsigned*>(dyn_lds);
-    int* const wf = reinterpret_cast<int*>(stack + S.stack_need * BLOCK);
+    int* const stack = reinterpret_cast<int*>(dyn_lds);
+    int* const wf = stack + S.stack_need * BLOCK;
     uint4* const blob = reinterpret_cast<uint4*>(wf + 3 * NP) + 3 * NP + NP / 4;
     DScene L = S;
     if (LDSM) {
@@ -2573,15 +2504,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     // traversal stack entries carry a 24-bit node / instance index (IDX_MASK)
     if (nodes.size() > IDX_MASK || (size_t)scene->ninstances > IDX_MASK)
         return bail(jt::fail(JT_ERR_UNSUPPORTED, "scene exceeds 2^24 BVH nodes or instances"));
-    // pre-tested child entries of HBM-mode stacks carry a 23-bit start and a 3-bit leaf count
-    if (nodes.size() > START_MASK || prims.size() / 4 > START_MASK || tlas_prims.size() > START_MASK)
-        return bail(jt::fail(JT_ERR_UNSUPPORTED, "scene exceeds 2^23 BVH nodes, primitive records or TLAS entries"));
-    for (const DNode& n : nodes) {
-        unsigned meta;
-        std::memcpy(&meta, &n.b.w, 4);
-        if ((meta >> 24) == 0 && (meta & 0xffffu) > 7u)
-            return bail(jt::fail(JT_ERR_UNSUPPORTED, "a BVH leaf holds more than 7 primitives (the reference's hold <= 4)"));
-    }
     if ((st = upload(c, nodes, &S.nodes)) || (st = upload(c, tlas_prims, &S.tlas_prims)) || (st = upload(c, prims, &S.prims)) ||
         (st = upload(c, itrav, &S.inst_trav)) || (st = upload(c, iblas, &S.inst_blas)) || (st = upload(c, ishade, &S.inst_shade)) ||
         (st = upload(c, shapes, &S.shapes)) || (st = upload(c, pos, &S.pos)) || (st = upload(c, nrm, &S.nrm)) ||
@@ -2631,8 +2553,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         // HBM mode's stack is the kernel's static ring (16 or 32 entries); LDS mode's, without
         // overflow, just the scene's bound
         const size_t acc_bytes = (size_t)ACC_SLOTS * BLOCK * 4;
-        // HBM mode: 64-bit stack entries, albedo / normal means in HBM (acc_slots(.., true))
-        const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 8 + (size_t)acc_slots(true, true) * BLOCK * 4;
+        const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 4 + acc_bytes;
         const size_t lds_base = (size_t)(c->stack <= 16 ? c->stack : c->ring) * BLOCK * 4 + acc_bytes;
         const size_t bytes = blob.size() * 16;
         const size_t lds_cu = 160 * 1024;
@@ -2671,10 +2592,10 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     }
     if (c->stack > 16) {  // HBM overflow of the LDS stack ring: `need` entries per pixel
         void* p = nullptr;
-        const size_t bytes = (size_t)W * (size_t)H * (size_t)need * 8;  // 64-bit entries in HBM mode
+        const size_t bytes = (size_t)W * (size_t)H * (size_t)need * 4;
         if ((e = hipMalloc(&p, bytes)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc stack overflow"));
         c->allocations.push_back(p);
-        S.ovf = p;
+        S.ovf = (int*)p;
         S.ovf_stride = need;
     }
 
