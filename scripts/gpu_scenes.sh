@@ -1,0 +1,16 @@
+# Configs 3-5 on one GPU: a bench line per scene at the stated size, and its roofline record
+# (kernel-trace + PMC passes of the same command). Config 3 runs at its spec; configs 4 and 5 are
+# 8-GPU configs, here on one GPU (config 5 at 64 of its 4096 spp).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/$1
+mkdir -p $O
+run() {  # <name> <workload> <bench args...>
+  local name=$1 wl=$2; shift 2
+  scripts/gpu_step.sh 600 $O/bench_$name.log timeout -k 10 580 python bench.py --no-cpu-baseline --steps 2 --warmup 1 "$@" || return 1
+  MEASURE_STEPS=1 MEASURE_WARMUP=0 bash scripts/gpu_measure.sh $O/$name "$wl" "$@" || return 1
+}
+run f2 "features2 path 1920x1080 512 samples/launch" --scene assets/scenes/features2/features2.json --width 1920 --height 1080 --spp 512 || exit 1
+run b1 "bathroom1 path 1920x1080 1024 samples/launch" --scene assets/scenes/bathroom1/bathroom1.json --width 1920 --height 1080 --spp 1024 || exit 1
+run ec "ecosys path 3840x2160 64 samples/launch" --scene assets/scenes/ecosys/ecosys.json --width 3840 --height 2160 --spp 64 || exit 1
