@@ -884,6 +884,8 @@ struct DAccum {
     unsigned* work;                // unit counters of the launch, one per XCD band at work[16 b]
                                    // (zeroed before each launch)
     int* tile_done;                // per 8x8 tile: sample chunks accumulated in this launch
+    float4* pool;                  // WF body: path-slot records (HBM), pool_bytes long
+    size_t pool_bytes;
 };
 
 // Work units: (sample chunk c, 8x8 pixel tile t), fetched by whole waves from atomic counters,
@@ -1209,9 +1211,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 // its order, and a pixel's samples are accumulated in order (one slot per pixel and chunk; the
 // chunks of a tile in order): results are bit-identical to trace_body.
 constexpr int WF_GMAX = 8;
-constexpr int WF_TRAV = 0, WF_SCENE = 1;
+constexpr int WF_TRAV = 0, WF_SCENE = 1, WF_LIGHT = 2;
 struct WfCtl {
-    unsigned head[3], tail[3];  // ring cursors: traversal, scene results ([2] unused; the block is read as 8 words)
+    unsigned head[3], tail[3];  // ring cursors
     unsigned attn;              // groups a wave should look at: idle while units remain, or waiting on a tile
     unsigned live;              // groups holding (or claiming) a unit
     int g_tile[WF_GMAX], g_uc[WF_GMAX], g_cs1[WF_GMAX];
@@ -1368,7 +1370,7 @@ __device__ __forceinline__ void wf_push(WfCtl& C, int* ring, int NP, int q, bool
 
 template <int SAMPLER, int COUNT, int F, bool NCACHE>
 __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A, int* stack,
-                              int* lds_wf) {
+                              int* lds_wf, float4* pool) {
     constexpr int RQ = wf_rec_q(F);
     const int lane = threadIdx.x & 63;
     const int G = P.wf_groups, NP = 64 * G;
@@ -1377,6 +1379,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     float4* const recs = reinterpret_cast<float4*>(lds_wf + 2 * NP);  // slot records (LDS)
     float4* const r_h = recs + (size_t)NP * RQ;                        // query hit: inst, elem, u, v
     float* const r_t = reinterpret_cast<float*>(r_h + NP);            // t
+    (void)pool;
     if (threadIdx.x < 3) {
         C.head[threadIdx.x] = 0;
         C.tail[threadIdx.x] = 0;
@@ -1792,7 +1795,7 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(D
 // queries / results, then the scene blob (LDS mode) or nothing (HBM mode: the scene from L2).
 template <int SAMPLER, int COUNT, int F, bool LDSM>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_WF void trace_kernel_wf(DScene S, DParams P, int s_begin, int s_end,
-                                                                            DAccum A) {
+                                                                            DAccum A, float4* pool) {
     extern __shared__ uint4 dyn_lds[];
     const int NP = 64 * P.wf_groups;
     int* const stack = reinterpret_cast<int*>(dyn_lds);
@@ -1805,7 +1808,7 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_WF void trace_kernel_wf(DSce
         L = blob_scene(S, blob);
     }
     L.nlnodes = 0;
-    trace_body_wf<SAMPLER, COUNT, F, !LDSM>(L, P, s_begin, s_end, A, stack + threadIdx.x, wf);
+    trace_body_wf<SAMPLER, COUNT, F, !LDSM>(L, P, s_begin, s_end, A, stack + threadIdx.x, wf, pool);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of
@@ -1852,9 +1855,9 @@ hipError_t launch_wf(const DScene& S, const DParams& P, int s0, int s1, const DA
     const int nwg = per_cu * cus;
     if (nwg < 1) return hipErrorInvalidValue;
     if (ldsm)
-        hipLaunchKernelGGL((trace_kernel_wf<SAMPLER, COUNT, F, true>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
+        hipLaunchKernelGGL((trace_kernel_wf<SAMPLER, COUNT, F, true>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A, A.pool);
     else
-        hipLaunchKernelGGL((trace_kernel_wf<SAMPLER, COUNT, F, false>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
+        hipLaunchKernelGGL((trace_kernel_wf<SAMPLER, COUNT, F, false>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A, A.pool);
     return hipGetLastError();
 }
 
@@ -2657,7 +2660,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, params->device) == hipSuccess && cus > 0) c->cus = cus;
     c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt,
-                  (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE};
+                  (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE, nullptr, 0};
     st = jt_reset(c);
     if (st != JT_OK) return bail(st);
     *out = c;
