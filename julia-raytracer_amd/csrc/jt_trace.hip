@@ -1222,15 +1222,11 @@ struct WfCtl {
     int exhausted;  // every band's units handed out
     int abort;      // a ring entry never arrived (never expected): every wave leaves, the launch fails
 };
-// A slot's record, in LDS (float4s): the path state that outlives a shading job (7; 9 with the
-// volume for FT_VOL) — sample_lights_pdf's chain (li, lcount, lq, pb, pdf, lpdf) never does,
-// since its instance queries run inline in the shading job — plus the pixel's image running
-// mean and hit count of this chunk. The albedo / normal means are read-modified-written in HBM.
-__host__ __device__ constexpr int wf_rec_q(int F) { return (F & FT_VOL) ? 9 : 7; }
-// LDS bytes per slot: two ring entries, the record, the query's hit (inst, elem, u, v; t)
-__host__ __device__ constexpr int wf_lds_slot(int F) { return 2 * 4 + 16 * wf_rec_q(F) + 16 + 4; }
-struct WfAcc {  // a slot's running means while it shades: image in the record, albedo / normal in HBM
+// float4s per slot record: path state (8), running means (3), the volume (2, FT_VOL)
+__host__ __device__ constexpr int wf_rec_q(int F) { return (F & FT_VOL) ? 13 : 11; }
+struct WfAcc {  // a slot's pixel running means (trace_body's acc slots), in registers while it shades
     float4 im;
+    v3 al, nr;
     int hits;
     float w;
 };
@@ -1244,16 +1240,21 @@ __device__ __forceinline__ void wf_store(float4* r, const Path& st, int pixel, i
                        __uint_as_float((unsigned)(c >> 32)));
     r[4] = make_float4(__int_as_float(st.bounce), __int_as_float(st.opbounce), __int_as_float(st.flags | st.phase << 8),
                        st.max_roughness);
-    r[5] = make_float4(__int_as_float(pixel), __int_as_float(sample), a.w, __int_as_float(a.hits));
-    r[6] = a.im;
+    r[5] = make_float4(__int_as_float(st.li), __int_as_float(st.lcount), st.pb, st.pdf);
+    r[6] = make_float4(st.lpdf, st.lq.x, st.lq.y, st.lq.z);
+    r[7] = make_float4(__int_as_float(pixel), __int_as_float(sample), a.w, __int_as_float(a.hits));
+    r[8] = a.im;
+    r[9] = make_float4(a.al.x, a.al.y, a.al.z, a.nr.x);
+    r[10] = make_float4(a.nr.y, a.nr.z, 0.0f, 0.0f);
     if (F & FT_VOL) {
-        r[7] = make_float4(st.vol.density.x, st.vol.density.y, st.vol.density.z, st.vol.scattering.x);
-        r[8] = make_float4(st.vol.scattering.y, st.vol.scattering.z, st.vol.scanisotropy, 0.0f);
+        r[11] = make_float4(st.vol.density.x, st.vol.density.y, st.vol.density.z, st.vol.scattering.x);
+        r[12] = make_float4(st.vol.scattering.y, st.vol.scattering.z, st.vol.scanisotropy, 0.0f);
     }
 }
 template <int F>
 __device__ __forceinline__ void wf_load(const float4* r, Path& st, int& pixel, int& sample, WfAcc& a) {
-    const float4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6];
+    const float4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6], q7 = r[7];
+    const float4 q8 = r[8], q9 = r[9], q10 = r[10];
     st.o = V3(q0.x, q0.y, q0.z);
     st.d = V3(q0.w, q1.x, q1.y);
     st.radiance = V3(q1.z, q1.w, q2.x);
@@ -1265,42 +1266,41 @@ __device__ __forceinline__ void wf_load(const float4* r, Path& st, int& pixel, i
     st.flags = __float_as_int(q4.z) & 0xff;
     st.phase = __float_as_int(q4.z) >> 8;
     st.max_roughness = q4.w;
-    pixel = __float_as_int(q5.x);
-    sample = __float_as_int(q5.y);
-    a.w = q5.z;
-    a.hits = __float_as_int(q5.w);
-    a.im = q6;
+    st.li = __float_as_int(q5.x);
+    st.lcount = __float_as_int(q5.y);
+    st.pb = q5.z;
+    st.pdf = q5.w;
+    st.lpdf = q6.x;
+    st.lq = V3(q6.y, q6.z, q6.w);
+    pixel = __float_as_int(q7.x);
+    sample = __float_as_int(q7.y);
+    a.w = q7.z;
+    a.hits = __float_as_int(q7.w);
+    a.im = q8;
+    a.al = V3(q9.x, q9.y, q9.z);
+    a.nr = V3(q9.w, q10.x, q10.y);
     if (F & FT_VOL) {
-        const float4 v0 = r[7], v1 = r[8];
+        const float4 v0 = r[11], v1 = r[12];
         st.vol.density = V3(v0.x, v0.y, v0.z);
         st.vol.scattering = V3(v0.w, v1.x, v1.y);
         st.vol.scanisotropy = v1.z;
     }
 }
 
-// the WF body's AOV accessor: the pixel's albedo / normal running means read-modified-written in
-// HBM (one owning slot per pixel and chunk; the same float operations as aov_update's LDS form)
+// the WF body's AOV accessor: the slot's running means in registers (same float operations as
+// aov_update's LDS form)
 struct WfAov {
     WfAcc* acc;
-    float4* albedo;
-    float4* normal;
-    int pixel;
     template <int F>
     __device__ __forceinline__ float w() const { return acc->w; }
 };
 template <int F>
 __device__ __forceinline__ void aov_update(const WfAov& a, v3 ta, v3 tn) {
-    const float aw = a.acc->w;
+    WfAcc& c = *a.acc;
+    const float aw = c.w;
     const float omw = 1 - aw;
-    float4 al = a.albedo[a.pixel], nr = a.normal[a.pixel];
-    al.x = al.x * omw + ta.x * aw;
-    al.y = al.y * omw + ta.y * aw;
-    al.z = al.z * omw + ta.z * aw;
-    nr.x = nr.x * omw + tn.x * aw;
-    nr.y = nr.y * omw + tn.y * aw;
-    nr.z = nr.z * omw + tn.z * aw;
-    a.albedo[a.pixel] = al;
-    a.normal[a.pixel] = nr;
+    c.al = V3(c.al.x * omw + ta.x * aw, c.al.y * omw + ta.y * aw, c.al.z * omw + ta.z * aw);
+    c.nr = V3(c.nr.x * omw + tn.x * aw, c.nr.y * omw + tn.y * aw, c.nr.z * omw + tn.z * aw);
 }
 
 __device__ __forceinline__ int lane_rank(unsigned long long m) {  // active lanes of m below this lane
@@ -1375,11 +1375,12 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     const int lane = threadIdx.x & 63;
     const int G = P.wf_groups, NP = 64 * G;
     __shared__ WfCtl C;
-    int* const ring[2] = {lds_wf, lds_wf + NP};
-    float4* const recs = reinterpret_cast<float4*>(lds_wf + 2 * NP);  // slot records (LDS)
-    float4* const r_h = recs + (size_t)NP * RQ;                        // query hit: inst, elem, u, v
-    float* const r_t = reinterpret_cast<float*>(r_h + NP);            // t
-    (void)pool;
+    int* const ring[3] = {lds_wf, lds_wf + NP, lds_wf + 2 * NP};
+    float4* const q_o = reinterpret_cast<float4*>(lds_wf + 3 * NP);  // o.xyz, root bits
+    float4* const q_d = q_o + NP;                                       // d.xyz
+    float4* const r_h = q_d + NP;                                       // inst, elem, u, v
+    float* const r_t = reinterpret_cast<float*>(r_h + NP);              // t
+    float4* const recs = pool + (size_t)blockIdx.x * NP * RQ;
     if (threadIdx.x < 3) {
         C.head[threadIdx.x] = 0;
         C.tail[threadIdx.x] = 0;
@@ -1392,7 +1393,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
         C.exhausted = 0;
         C.abort = 0;
     }
-    for (int k = threadIdx.x; k < 2 * NP; k += BLOCK) lds_wf[k] = -1;
+    for (int k = threadIdx.x; k < 3 * NP; k += BLOCK) lds_wf[k] = -1;
     __syncthreads();
 
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
@@ -1417,8 +1418,17 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
 #define WF_ADD(k, v) ((void)0)
 #endif
 
-    // a slot's pending closest-hit query is its record's ray (st.o, st.d)
-    auto issue = [&](int, const Path&) { cnt.rays++; };
+    // a slot's pending query (LDS): origin, direction, root
+    auto issue = [&](int s, const Path& st) {
+        const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
+        const v3 o = light ? st.lq : st.o;
+        const unsigned root = light ? (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance
+                                    : (T_TLAS << 30) | SNAP_NONE;
+        q_o[s] = make_float4(o.x, o.y, o.z, __uint_as_float(root));
+        q_d[s] = make_float4(st.d.x, st.d.y, st.d.z, 0.0f);
+        if (light) cnt.light_queries++;
+        else cnt.rays++;
+    };
 
     // Roles: the last P.wf_shaders waves of the workgroup only shade and start slot groups; the
     // others traverse, refilling their lanes from the ring, and shade too whenever they hold no
@@ -1462,9 +1472,9 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                         const int r = lane_rank(__builtin_amdgcn_ballot_w64(qslot < 0));
                         if (qslot < 0 && r < n) {
                             const int s = wf_take(C, ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
-                            const float4 q0 = recs[(size_t)s * RQ], q1 = recs[(size_t)s * RQ + 1];
+                            const float4 o = q_o[s], d = q_d[s];
                             qslot = s;
-                            query_begin(T, V3(q0.x, q0.y, q0.z), V3(q0.w, q1.x, q1.y), (T_TLAS << 30) | SNAP_NONE, stack);
+                            query_begin(T, V3(o.x, o.y, o.z), V3(d.x, d.y, d.z), __float_as_uint(o.w), stack);
 #pragma unroll
                             for (int k = 0; k < JT_FIRST_POP; k++)
                                 if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
@@ -1585,7 +1595,8 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             const int cs0 = s_begin + uc * P.chunk;
             const int pixel = j * P.width + i;
             if (in_image) {
-                WfAcc acc{A.image[pixel], 0, 1.0f / (float)(cs0 - P.first + 1)};
+                const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
+                WfAcc acc{im, V3(al.x, al.y, al.z), V3(nr.x, nr.y, nr.z), 0, 1.0f / (float)(cs0 - P.first + 1)};
                 Path st;
                 start_path(P, i, j, pixel, cs0, st);
                 wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0, acc);
@@ -1628,7 +1639,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
             const float4 hh = r_h[s];
             const Hit h{__float_as_int(hh.x), __float_as_int(hh.y), hh.z, hh.w, r_t[s], __float_as_int(hh.x) >= 0};
-            const WfAov aov{&acc, A.albedo, A.normal, pixel};
+            const WfAov aov{&acc};
             bool done;
             if (SAMPLER == 2) done = naive_hit<F>(S, P, st, h, aov, cnt.shades);
             else done = path_hit<F>(S, P, st, h, aov, cnt.shades);
@@ -1667,6 +1678,8 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                 } else {  // the slot's chunk is done: its pixel's running means back to HBM
                     alive = false;
                     A.image[pixel] = acc.im;
+                    A.albedo[pixel] = make_float4(acc.al.x, acc.al.y, acc.al.z, 0.0f);
+                    A.normal[pixel] = make_float4(acc.nr.x, acc.nr.y, acc.nr.z, 0.0f);
                     A.hits[pixel] += acc.hits;
                 }
             }
@@ -1731,7 +1744,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
 #endif
 // WF kernels (trace_body_wf): occupancy request, 0 = the compiler's choice
 #ifndef JT_WAVES_WF
-#define JT_WAVES_WF 2  // the slot records in LDS allow 2 workgroups per CU: registers are free
+#define JT_WAVES_WF 4
 #endif
 #if JT_WAVES_WF > 0
 #define JT_WAVES_PER_EU_WF __attribute__((amdgpu_waves_per_eu(JT_WAVES_WF, JT_WAVES_WF)))
@@ -1800,7 +1813,7 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_WF void trace_kernel_wf(DSce
     const int NP = 64 * P.wf_groups;
     int* const stack = reinterpret_cast<int*>(dyn_lds);
     int* const wf = stack + S.stack_need * BLOCK;
-    uint4* const blob = reinterpret_cast<uint4*>(reinterpret_cast<char*>(wf) + (size_t)NP * wf_lds_slot(F));
+    uint4* const blob = reinterpret_cast<uint4*>(wf + 3 * NP) + 3 * NP + NP / 4;
     DScene L = S;
     if (LDSM) {
         for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
@@ -1845,14 +1858,16 @@ template <int SAMPLER, int COUNT, int F>
 hipError_t launch_wf(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
     const int NP = 64 * P.wf_groups;
     const bool ldsm = S.blob_n16 > 0;
-    const size_t lds = (size_t)S.stack_need * BLOCK * 4 + (size_t)NP * wf_lds_slot(F) + (ldsm ? (size_t)S.blob_n16 * 16 : 0);
+    const size_t lds = (size_t)S.stack_need * BLOCK * 4 + (size_t)NP * (3 * 4 + 3 * 16 + 4) +
+                       (ldsm ? (size_t)S.blob_n16 * 16 : 0);
     const void* k = ldsm ? (const void*)trace_kernel_wf<SAMPLER, COUNT, F, true>
                          : (const void*)trace_kernel_wf<SAMPLER, COUNT, F, false>;
     hipError_t e;
     if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-    const int nwg = per_cu * cus;
+    const size_t rec = (size_t)NP * wf_rec_q(F) * 16;
+    const int nwg = (int)std::min<size_t>((size_t)per_cu * cus, A.pool_bytes / rec);
     if (nwg < 1) return hipErrorInvalidValue;
     if (ldsm)
         hipLaunchKernelGGL((trace_kernel_wf<SAMPLER, COUNT, F, true>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A, A.pool);
@@ -2627,7 +2642,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.wf_groups = 0;
     if (const char* wf = std::getenv("JT_WF")) {
         if (std::atoi(wf) > 0 && c->stack <= 16) {
-            P.wf_groups = 6;
+            P.wf_groups = 5;
             if (const char* g = std::getenv("JT_WF_GROUPS")) P.wf_groups = std::max(1, std::min(WF_GMAX, std::atoi(g)));
             P.wait_lanes = 56;
             if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
@@ -2661,6 +2676,14 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, params->device) == hipSuccess && cus > 0) c->cus = cus;
     c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt,
                   (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE, nullptr, 0};
+    if (P.wf_groups > 0) {  // path-slot records: at most 8 workgroups of 256 lanes per CU
+        const size_t bytes = (size_t)c->cus * 8 * 64 * WF_GMAX * wf_rec_q(FT_ALL) * 16;
+        void* pool = nullptr;
+        if ((e = hipMalloc(&pool, bytes)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc WF path records"));
+        c->allocations.push_back(pool);
+        c->A.pool = (float4*)pool;
+        c->A.pool_bytes = bytes;
+    }
     st = jt_reset(c);
     if (st != JT_OK) return bail(st);
     *out = c;
