@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef JT_SLAB_FAST
+#define JT_SLAB_FAST 0
+#endif
 #ifndef JT_EXACT_MATH
 #define JT_EXACT_MATH 1
 #endif
@@ -84,7 +87,9 @@ struct alignas(16) DLight {
     // guide_t[k] (float) and guide_a[k] = first 0-based index i with cdf[i] > guide_t[k]
     int guide_offset, nguide;
     float guide_scale;  // nguide / last(cdf): first guess of the bucket of a limit
-    int pad;
+    // JT_ENV_ALIAS=1 (statistical variant, not the default): offset of an environment light's
+    // Vose alias table in DScene::alias (ncdf entries), -1 = none
+    int alias_offset;
 };
 
 struct DScene {
@@ -115,6 +120,7 @@ struct DScene {
     const float* cdf;
     const float* guide_t;   // DLight guide tables (thresholds / first indices)
     const int* guide_a;
+    const float2* alias;    // DLight alias tables: (keep probability, alias index bits) per texel
     const float* srgb_lut;  // srgb_to_rgb(byte_to_float(b)), 256 entries (src/color.jl:12-23)
     const float* byte_lut;  // byte_to_float(b)
     int tlas_nnodes, nenvs, nlights, pad;
@@ -497,6 +503,27 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
     return r;
 }
 
+// The slab test's final compare, `t1 *= 1.00000024; t0 <= t1` (src/geometry.jl:102-103): the
+// Float32 t1 is promoted, so the product and the compare are Float64.
+__device__ __forceinline__ bool slab_pass(float t0, float t1) {
+#if JT_SLAB_FAST
+    // Decided in float where that is exact; callers guarantee t0 >= tmin > 0 (t0 is a max with
+    // ray_eps) for non-NaN slabs. t0 <= t1 implies t0 <= t1*c (c > 1, t1 > 0). t0 > RN_f(t1 * k),
+    // k = 1 + 5*2^-23, implies t0 > RN_d(t1*c), since k(1 - 2^-24) > c(1 + 2^-53) for t1 > 0 (a
+    // denormal, zero or negative t1 is below tmin either way). Only t1 < t0 <= RN_f(t1 k), a few
+    // ulps, takes the double compare, behind a wave-uniform branch.
+    // scripts/exhaustive/slab_check.hip checks this against the double compare for every t1.
+    bool pass = t0 <= t1;
+    const bool amb = !pass && t0 <= t1 * 1.0000006f;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(amb) != 0, 0)) {
+        if (amb) pass = (double)t0 <= (double)t1 * 1.00000024;
+    }
+    return pass;
+#else
+    return (double)t0 <= (double)t1 * 1.00000024;
+#endif
+}
+
 // intersect_bbox (src/geometry.jl:96-105): Julia min/max; `t1 *= 1.00000024` is Float64.
 // Any NaN slab value makes Julia's t0 or t1 NaN and culls the box; that case is tested
 // separately, so the min/max chains below only ever see non-NaN values, where IEEE min/max
@@ -514,7 +541,7 @@ __device__ __forceinline__ bool intersect_bbox(v3 o, v3 dinv, float tmin, float 
                __builtin_isnan(My) | __builtin_isnan(Mz);
     float t0 = vmax3(vmin(mx, Mx), vmin(my, My), vmax(vmin(mz, Mz), tmin));
     float t1 = vmin3(vmax(mx, Mx), vmax(my, My), vmin(vmax(mz, Mz), tmax));
-    return !nan && ((double)t0 <= (double)t1 * 1.00000024);
+    return !nan && slab_pass(t0, t1);
 }
 
 struct PrimHit {

@@ -525,9 +525,20 @@ __device__ __forceinline__ v3 sample_lights(const DScene& S, v3 position, float 
     if ((F & FT_ENV) && l.environment >= 0) {
         const DEnv& env = S.envs[l.environment];
         const DTexture t = S.textures[env.tex];
-        const int idx = l.nguide ? sample_discrete_guided(cdf, l.ncdf, rel, S.guide_t + l.guide_offset,
-                                                          S.guide_a + l.guide_offset, l.nguide, l.guide_scale)
-                                 : sample_discrete(cdf, l.ncdf, rel);  // 1-based, used as-is (:990-993)
+        int idx;  // 1-based, used as-is (:990-993)
+        if (l.alias_offset >= 0) {
+            // alias-table variant (JT_ENV_ALIAS=1): O(1) — column from rel,
+            // keep-or-alias coin from ruv.x (an environment sample does not use ruv). It samples
+            // the pmf the CDF holds, so env_light_pdf is unchanged, but it maps random numbers to
+            // texels differently from upper_bound: statistically equal, not bit-exact.
+            const int col = jl_clampi((int)(rel * (float)l.ncdf), 0, l.ncdf - 1);
+            const float2 a = S.alias[l.alias_offset + col];
+            idx = (ruv.x < a.x ? col : __float_as_int(a.y)) + 1;
+        } else {
+            idx = l.nguide ? sample_discrete_guided(cdf, l.ncdf, rel, S.guide_t + l.guide_offset,
+                                                    S.guide_a + l.guide_offset, l.nguide, l.guide_scale)
+                           : sample_discrete(cdf, l.ncdf, rel);
+        }
         float u = ((float)(idx % t.width) + 0.5f) / (float)t.width;
         float v = (float)((((double)idx / (double)t.width) + 0.5) / (double)t.height);
         float su, cu, sv, cv;
@@ -1948,6 +1959,7 @@ struct jt_ctx {
     int first = -1, next = 0;  // running-mean origin and next expected sample
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     bool failed = false;       // a launch's tile-order wait timed out: the running means are unusable
+    bool env_alias = false;    // JT_ENV_ALIAS=1: environment lights sample through alias tables
                                // until jt_reset
     size_t lds_scene_bytes = 0;  // > 0: small-scene LDS mode
     unsigned long long launches = 0;
@@ -2003,6 +2015,42 @@ const Rccl& rccl() {
 }
 int nccl_fail(ncclResult_t r, const char* what) {
     return jt::fail(JT_ERR_DEVICE, std::string(what) + ": " + rccl().GetErrorString(r));
+}
+
+// Vose's alias table of the pmf a light CDF holds (p_i = cdf[i] - cdf[i-1], src/sampling.jl:39-40),
+// appended to `out`: entry i = (probability of keeping column i, the other index of the column).
+// Built in double; the JT_ENV_ALIAS variant's sample_lights reads it.
+void build_alias_table(const float* cdf, int n, std::vector<float2>& out) {
+    auto bits = [](int i) {
+        float f;
+        std::memcpy(&f, &i, 4);
+        return f;
+    };
+    std::vector<double> q(n);
+    double total = 0;
+    for (int i = 0; i < n; i++) {
+        q[i] = std::max(0.0, (double)cdf[i] - (i ? (double)cdf[i - 1] : 0.0));
+        total += q[i];
+    }
+    const size_t base = out.size();
+    out.resize(base + n);
+    std::vector<int> small, large;
+    for (int i = 0; i < n; i++) {
+        q[i] = total > 0 ? q[i] * n / total : 1.0;
+        (q[i] < 1.0 ? small : large).push_back(i);
+    }
+    while (!small.empty() && !large.empty()) {
+        const int s = small.back(), l = large.back();
+        small.pop_back();
+        out[base + s] = make_float2((float)q[s], bits(l));
+        q[l] -= 1.0 - q[s];
+        if (q[l] < 1.0) {
+            large.pop_back();
+            small.push_back(l);
+        }
+    }
+    for (int i : large) out[base + i] = make_float2(1.0f, bits(i));
+    for (int i : small) out[base + i] = make_float2(1.0f, bits(i));  // rounding leftovers
 }
 
 template <class T>
@@ -2471,9 +2519,13 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     std::vector<DLight> dl(lights->nlights);
     std::vector<float> cdf, guide_t;
     std::vector<int> guide_a;
+    std::vector<float2> alias;
+    const char* ea = std::getenv("JT_ENV_ALIAS");
+    const bool env_alias = ea && std::atoi(ea) != 0;
+    c->env_alias = env_alias;
     for (int k = 0; k < lights->nlights; k++) {
         const jt_light& l = lights->lights[k];
-        dl[k] = DLight{l.instance, l.environment, (int)cdf.size(), l.ncdf, 0, 0, 0.0f, 0};
+        dl[k] = DLight{l.instance, l.environment, (int)cdf.size(), l.ncdf, 0, 0, 0.0f, -1};
         cdf.insert(cdf.end(), l.cdf, l.cdf + l.ncdf);
         const float last = l.ncdf > 0 ? l.cdf[l.ncdf - 1] : 0.0f;
         bool monotone = true;
@@ -2490,6 +2542,10 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                 const int a = (int)(std::upper_bound(l.cdf, l.cdf + l.ncdf, t) - l.cdf);
                 guide_t.push_back(t);
                 guide_a.push_back(a);
+            }
+            if (env_alias && l.environment >= 0) {
+                dl[k].alias_offset = (int)alias.size();
+                build_alias_table(l.cdf, l.ncdf, alias);
             }
         }
     }
@@ -2511,7 +2567,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, enrm, &S.enrm)) || (st = upload(c, enrm_id, &S.enrm_id)) ||
         (st = upload(c, mats, &S.materials)) || (st = upload(c, texs, &S.textures)) || (st = upload(c, texb, &S.texb)) ||
         (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) ||
-        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
+        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
         return bail(st);
     S.tlas_nnodes = (int)tlas.size();
     S.nenvs = scene->nenvironments;
@@ -3065,10 +3121,11 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     char tmp[512];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d light_lanes=%d chunk=%d tiles=%d block=%d wf_groups=%d",
+                  "wait_lanes=%d light_lanes=%d chunk=%d tiles=%d block=%d wf_groups=%d env_alias=%d",
                   c->P.wf_groups ? "trace_kernel_wf" : c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, c->kmask, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
-                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->tiles, BLOCK, c->P.wf_groups);
+                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->tiles, BLOCK, c->P.wf_groups,
+                  c->env_alias ? 1 : 0);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;
 }

@@ -1,0 +1,59 @@
+"""Environment-light alias tables (JT_ENV_ALIAS=1; SURVEY §8(f) rank 3, src/trace.jl:968-1008 and
+src/sampling.jl:33-56): an O(1) Vose alias draw replaces upper_bound over the environment CDF.
+It samples the same pmf but maps random numbers to texels differently, so it cannot be
+bit-exact with the reference's upper_bound: it is a non-default statistical variant. Checked
+here (1) against the reference's own renders through the same block-mean pins as the default
+path (tests/test_gpu_scenes.py::test_statistical_pin_reference_render), and (2) against the
+default (bit-exact, oracle-checked) path at equal sample counts: channel means and ray counts
+within noise, images not identical (the variant really ran)."""
+import numpy as np
+import pytest
+
+from conftest import make_params
+import test_gpu_scenes as tgs
+from test_gpu_scenes import scene_abi
+
+pytestmark = pytest.mark.gpu
+
+
+def _render(abi, lib, sa, p, spp, alias, monkeypatch):
+    from jtrace import trace
+    if alias:
+        monkeypatch.setenv("JT_ENV_ALIAS", "1")
+    else:
+        monkeypatch.delenv("JT_ENV_ALIAS", raising=False)
+    bvh = trace.make_scene_bvh(sa, False, lib)
+    lights = trace.make_trace_lights(sa, lib)
+    st = trace.make_trace_state(sa, bvh, lights, p, lib)
+    st.trace_range(0, spp)
+    out = (st.get_image(), st.counters(), st.describe())
+    st.close()
+    return out
+
+
+@pytest.mark.parametrize("name", ["features1", "features2"])
+def test_alias_pin_reference_render(gpu, abi, lib, monkeypatch, name):
+    monkeypatch.setenv("JT_ENV_ALIAS", "1")
+    tgs.test_statistical_pin_reference_render(gpu, abi, lib, name, 1)
+
+
+@pytest.mark.parametrize("name", ["features1", "ecosys"])
+def test_alias_matches_default_path_statistically(gpu, abi, lib, monkeypatch, name):
+    sa = scene_abi(name)
+    spp = 64
+    p = make_params(abi, resolution=128, samples=spp, batch=spp)
+    ref = _render(abi, lib, sa, p, spp, False, monkeypatch)
+    ali = _render(abi, lib, sa, p, spp, True, monkeypatch)
+    assert "env_alias=0" in ref[2] and "env_alias=1" in ali[2], (ref[2], ali[2])
+    assert not np.array_equal(ref[0], ali[0])
+    cm_r = ref[0][..., :3].reshape(-1, 3).mean(axis=0)
+    cm_a = ali[0][..., :3].reshape(-1, 3).mean(axis=0)
+    print(name, "channel means default", cm_r, "alias", cm_a, "rays", ref[1]["rays"], ali[1]["rays"])
+    np.testing.assert_allclose(cm_a, cm_r, rtol=0.01)
+    # 16x16-pixel block means (256 pixels x 64 spp each) agree to a few per cent
+    h, w = ref[0].shape[:2]
+    b = 16
+    bm = lambda im: im[: h // b * b, : w // b * b, :3].reshape(h // b, b, w // b, b, 3).mean(axis=(1, 3))
+    rel = np.abs(bm(ali[0]) - bm(ref[0])) / np.maximum(bm(ref[0]), 0.02)
+    assert np.median(rel) < 0.02, np.median(rel)
+    assert abs(ali[1]["rays"] - ref[1]["rays"]) <= 0.01 * ref[1]["rays"]
