@@ -133,6 +133,9 @@ struct DScene {
     // into LDS by every workgroup and read from there (lnodes)
     const DNode* lnodes;
     int nlnodes;
+    // HBM mode, JT_POP_LDS: one LDS record per lane (node index, start, meta) of the child the
+    // last pre-test pushed (set by the kernel; nullptr elsewhere)
+    uint4* pcl;
     // traversal-stack overflow (scenes deeper than the LDS ring): ovf_stride entries per pixel
     int* ovf;
     int ovf_stride;

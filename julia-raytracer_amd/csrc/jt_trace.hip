@@ -38,6 +38,12 @@
 #ifndef JT_FIRST_POP
 #define JT_FIRST_POP 1
 #endif
+#ifndef JT_POP_CACHE
+#define JT_POP_CACHE 0
+#endif
+#ifndef JT_POP_LDS
+#define JT_POP_LDS 0
+#endif
 #ifndef JT_CHILD_PRETEST
 #define JT_CHILD_PRETEST 1
 #endif
@@ -294,6 +300,11 @@ struct Trav {
     int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
     float h_u, h_v;
     int nh;              // hits accepted so far (every tmax change), saturating at 63
+    // JT_POP_CACHE (HBM mode): start/meta words of the child the last pre-test pushed — the
+    // next pop when the lane's next step is a pop — so that pop loads nothing (node records
+    // are immutable: a cached index always maps to its own words)
+    unsigned pc_idx;
+    float pc_start, pc_meta;
 };
 
 __device__ __forceinline__ int neg_mask(v3 d) { return (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0); }
@@ -334,6 +345,7 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     stack[0] = (int)root;
     T.sp = 1;
     T.low = 0;
+    T.pc_idx = ~0u;
 }
 
 // The current BLAS leaf's next primitive(s), in order (src/bvh.jl:444-484). Triangles go in
@@ -464,7 +476,15 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
     const unsigned snap = (e >> 24) & 63u;
     float4 nb;
     if (NCACHE && snap != 63u && snap == (unsigned)T.nh) {
-        nb = ((int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
+        if (JT_POP_CACHE && idx == T.pc_idx) {
+            nb = make_float4(0.0f, 0.0f, T.pc_start, T.pc_meta);  // z, w only
+        } else if (JT_POP_LDS) {
+            const uint4 pc = S.pcl[threadIdx.x];
+            if (pc.x == idx) nb = make_float4(0.0f, 0.0f, __uint_as_float(pc.y), __uint_as_float(pc.z));
+            else nb = ((int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
+        } else {
+            nb = ((int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
+        }
     } else {
         const DNode nd = (NCACHE && (int)idx < S.nlnodes) ? S.lnodes[idx] : S.nodes[idx];
         if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
@@ -493,6 +513,14 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             const unsigned ptag = type << 30 | (unsigned)T.nh << 24;  // pre-tested at hit count nh
             if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_far);
             if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_near);
+            if (JT_POP_LDS && (k0 || k1))
+                S.pcl[threadIdx.x] = make_uint4(k1 ? c_near : c_far, __float_as_uint(k1 ? n1.b.z : n0.b.z),
+                                                __float_as_uint(k1 ? n1.b.w : n0.b.w), 0u);
+            if (JT_POP_CACHE) {  // the child pushed last is popped next if this lane pops next
+                T.pc_idx = k1 ? c_near : (k0 ? c_far : T.pc_idx);
+                T.pc_start = k1 ? n1.b.z : (k0 ? n0.b.z : T.pc_start);
+                T.pc_meta = k1 ? n1.b.w : (k0 ? n0.b.w : T.pc_meta);
+            }
         } else {
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_far);
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_near);
@@ -660,6 +688,9 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
 // state parked in LDS instead of registers kept live (and spilled) across the traversal loop.
 #ifndef JT_LANE_LDS
 #define JT_LANE_LDS 1
+#endif
+#ifndef JT_ACC_HBM
+#define JT_ACC_HBM 0
 #endif
 // Not in the FT_NONE kernels: cornellbox's LDS-mode kernel then no longer fits 5 workgroups per
 // CU (-9 %); the mesh kernels gain (features2 +7 %, bathroom1 +1 %, ecosys +0.6 %).
@@ -940,8 +971,11 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     constexpr bool LL = lane_lds(F);
-    __shared__ float acc_lds[(LL ? 13 : 11) * BLOCK];
-    float* acc = acc_lds + threadIdx.x;
+    // JT_ACC_HBM (experiment, FT_NONE kernels): the running-mean slots in a per-lane HBM (L2)
+    // area instead of LDS, so more workgroups fit per CU
+    constexpr bool AH = JT_ACC_HBM && !LL;
+    __shared__ float acc_lds[AH ? 1 : (LL ? 13 : 11) * BLOCK];
+    float* acc = AH ? reinterpret_cast<float*>(A.pool) + (size_t)blockIdx.x * 11 * BLOCK + threadIdx.x : acc_lds + threadIdx.x;
 #if JT_STAMPS
     unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
     unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
@@ -1793,12 +1827,15 @@ __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob)
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     __shared__ int lds_stack[RING * BLOCK];
+    __shared__ uint4 pop_lds[JT_POP_LDS ? BLOCK : 1];
     extern __shared__ uint4 node_cache[];
     const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
     for (int k = threadIdx.x; k < 2 * S.nlnodes; k += BLOCK) node_cache[k] = src[k];
+    if (JT_POP_LDS) pop_lds[threadIdx.x] = make_uint4(~0u, 0u, 0u, 0u);
     __syncthreads();
     DScene L = S;
     L.lnodes = reinterpret_cast<const DNode*>(node_cache);
+    L.pcl = pop_lds;
     trace_body<SAMPLER, RING, OVF, COUNT, F, true>(L, P, s_begin, s_end, A, lds_stack + threadIdx.x);
 }
 
@@ -1832,6 +1869,11 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_WF void trace_kernel_wf(DSce
         L = blob_scene(S, blob);
     }
     L.nlnodes = 0;
+    __shared__ uint4 pop_lds[JT_POP_LDS ? BLOCK : 1];
+    if (JT_POP_LDS) {
+        pop_lds[threadIdx.x] = make_uint4(~0u, 0u, 0u, 0u);
+        L.pcl = pop_lds;
+    }
     trace_body_wf<SAMPLER, COUNT, F, !LDSM>(L, P, s_begin, s_end, A, stack + threadIdx.x, wf, pool);
 }
 
@@ -1913,7 +1955,10 @@ hipError_t launch_s(int need, int ring, int kmask, const DScene& S, const DParam
     (void)need;
     (void)ring;
     (void)kmask;
-    return launch_t<1, 16, false, 0, JT_ONE_FEAT>(S, P, s0, s1, A, st, cus);
+#ifndef JT_ONE_OVF
+#define JT_ONE_OVF false
+#endif
+    return launch_t<1, 16, JT_ONE_OVF, 0, JT_ONE_FEAT, !JT_ONE_OVF>(S, P, s0, s1, A, st, cus);
 #else
     if (need <= 16) {
         if (P.wf_groups > 0) {
@@ -2609,7 +2654,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         // HBM mode's stack is the kernel's static ring (16 or 32 entries); LDS mode's, without
         // overflow, just the scene's bound
         const size_t acc_bytes = (size_t)ACC_SLOTS * BLOCK * 4;
-        const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 4 + acc_bytes;
+        const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 4 + acc_bytes +
+                                  (JT_POP_LDS ? (size_t)BLOCK * 16 : 0);
         const size_t lds_base = (size_t)(c->stack <= 16 ? c->stack : c->ring) * BLOCK * 4 + acc_bytes;
         const size_t bytes = blob.size() * 16;
         const size_t lds_cu = 160 * 1024;
@@ -2732,6 +2778,14 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, params->device) == hipSuccess && cus > 0) c->cus = cus;
     c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt,
                   (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE, nullptr, 0};
+    if (JT_ACC_HBM && P.wf_groups == 0) {  // running-mean slots: at most 8 workgroups of 256 lanes per CU
+        const size_t bytes = (size_t)c->cus * 8 * 11 * BLOCK * 4;
+        void* pool = nullptr;
+        if ((e = hipMalloc(&pool, bytes)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc running-mean slots"));
+        c->allocations.push_back(pool);
+        c->A.pool = (float4*)pool;
+        c->A.pool_bytes = bytes;
+    }
     if (P.wf_groups > 0) {  // path-slot records: at most 8 workgroups of 256 lanes per CU
         const size_t bytes = (size_t)c->cus * 8 * 64 * WF_GMAX * wf_rec_q(FT_ALL) * 16;
         void* pool = nullptr;
