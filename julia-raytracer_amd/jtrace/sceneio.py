@@ -18,7 +18,6 @@ from __future__ import annotations
 import json
 import os
 import re
-import struct
 import warnings
 
 import numpy as np
@@ -387,6 +386,3 @@ def decode_srgb8(arr: np.ndarray) -> np.ndarray:
     c = arr.astype(np.float64) / 255.0
     return np.where(c <= 0.04045, c / 12.92, ((c + 0.055) / 1.055) ** 2.4)
 
-
-def struct_pack_check():  # pragma: no cover - keeps `struct` import meaningful for tooling
-    return struct.calcsize("<f")
