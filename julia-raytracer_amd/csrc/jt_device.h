@@ -14,6 +14,9 @@
 #ifndef JT_SLAB_FAST
 #define JT_SLAB_FAST 0
 #endif
+#ifndef JT_MAX_CHUNKS
+#define JT_MAX_CHUNKS 32
+#endif
 #ifndef JT_EXACT_MATH
 #define JT_EXACT_MATH 1
 #endif
@@ -164,6 +167,10 @@ struct DParams {
     int light_lanes;  // path sampler: run a light-hit step inside the traversal phase once this
                       // many lanes wait on a sample_lights_pdf query result (65: never)
     int chunk;  // samples per work unit (a tile's chunks run in order)
+    // chunk table (nct > 0): chunk c covers samples [s_begin + cbeg[c], s_begin + cbeg[c+1]) —
+    // full chunks, then a halving tail that shortens the launch's last units (JT_CHUNK_MIN)
+    int nct;
+    int cbeg[JT_MAX_CHUNKS + 1];
     int wf_groups;  // WF body: 64-slot path groups per workgroup
     int wf_refill;  // WF body: idle lanes that make a traversal step first take new queries
     int wf_shaders; // WF body: shading waves per workgroup (the others traverse)

@@ -955,6 +955,20 @@ __device__ __forceinline__ void publish_tile(const DAccum& A, int t, int c) {
     if ((threadIdx.x & 63) == 0) __hip_atomic_store(A.tile_done + t, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// sample range of chunk uc of a launch over [s_begin, s_end)
+__device__ __forceinline__ int num_chunks(const DParams& P, int s_begin, int s_end) {
+    return P.nct > 0 ? P.nct : (s_end - s_begin + P.chunk - 1) / P.chunk;
+}
+__device__ __forceinline__ void chunk_range(const DParams& P, int s_begin, int s_end, int uc, int& cs0, int& cs1) {
+    if (P.nct > 0) {
+        cs0 = s_begin + P.cbeg[uc];
+        cs1 = s_begin + P.cbeg[uc + 1];
+    } else {
+        cs0 = s_begin + uc * P.chunk;
+        cs1 = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
+    }
+}
+
 // lane id (0..63) recomputed where it is used: an asm the compiler cannot merge with an earlier one
 __device__ __forceinline__ int opaque_lane_id() {
     unsigned l;
@@ -981,7 +995,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
 #endif
     const int tiles_x = (P.width + 7) / 8, tiles = tiles_x * ((P.height + 7) / 8);
-    const int nchunks = (s_end - s_begin + P.chunk - 1) / P.chunk;
+    const int nchunks = num_chunks(P, s_begin, s_end);
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     int band_k = 0;
@@ -999,7 +1013,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     if (uc > 0) wait_tile(A, ut, uc);
     const int i = (ut % tiles_x) * 8 + (lane & 7);
     const int j = (ut / tiles_x) * 8 + (lane >> 3);
-    const int cs0 = s_begin + uc * P.chunk, cs1 = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
+    int cs0, cs1;
+    chunk_range(P, s_begin, s_end, uc, cs0, cs1);
     int pixel = j * P.width + i;
     bool in_image = i < P.width && j < P.height;
     bool alive = in_image;
@@ -1443,7 +1458,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
 
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     const int tiles_x = (P.width + 7) / 8, tiles = tiles_x * ((P.height + 7) / 8);
-    const int nchunks = (s_end - s_begin + P.chunk - 1) / P.chunk;
+    const int nchunks = num_chunks(P, s_begin, s_end);
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     Trav T;
@@ -1617,8 +1632,9 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
                     } else {
                         C.g_tile[g] = unit_t;
                         C.g_uc[g] = unit_uc;
-                        const int cs0 = s_begin + unit_uc * P.chunk;
-                        C.g_cs1[g] = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
+                        int cs0, cs1;
+                        chunk_range(P, s_begin, s_end, unit_uc, cs0, cs1);
+                        C.g_cs1[g] = cs1;
                         if (unit_uc > 0 &&
                             __hip_atomic_load(A.tile_done + unit_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unit_uc) {
                             // its tile's previous chunk is not published yet: start it later
@@ -1637,7 +1653,9 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             const int i = (ut % tiles_x) * 8 + (lane & 7), j = (ut / tiles_x) * 8 + (lane >> 3);
             const bool in_image = i < P.width && j < P.height;
             const int s = g * 64 + lane;
-            const int cs0 = s_begin + uc * P.chunk;
+            int cs0, cs1u;
+            chunk_range(P, s_begin, s_end, uc, cs0, cs1u);
+            (void)cs1u;
             const int pixel = j * P.width + i;
             if (in_image) {
                 const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
@@ -1996,6 +2014,7 @@ struct jt_ctx {
     int total_samples = 0, batch = 1, sampler = 1;
     int cus = 256;   // compute units of the device (persistent grid size)
     int chunk = 0;   // samples per work unit (0: chosen per launch)
+    int chunk_min = 0;  // > 0: the launch's chunk table ends with a halving tail down to this many samples
     int tiles = 0;   // 8x8 pixel tiles
     int stack = 16;  // stack bound of the scene (entries); > 16: LDS ring of `ring` + HBM overflow
     int ring = 16;
@@ -2728,6 +2747,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.chunk = 0;  // 0: per launch, a quarter of its samples within [8, 64] (enough units per wave)
     if (const char* ch = std::getenv("JT_CHUNK")) P.chunk = std::max(1, std::atoi(ch));
     c->chunk = P.chunk;
+    if (const char* cm = std::getenv("JT_CHUNK_MIN")) c->chunk_min = std::max(0, std::atoi(cm));
     // measured best (cornellbox): 40 waiting lanes per shading phase; 48 with
     // light-hit steps in the traversal phase (they take the light queries out of the phases)
     c->kmask = kernel_mask(c->feat, c->stack, c->ring, c->lds_scene_bytes > 0);
@@ -2894,6 +2914,21 @@ namespace {
 int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
     c->P.first = first;
     c->P.chunk = c->chunk > 0 ? c->chunk : std::max(8, std::min(64, (s1 - s0) / 4));
+    // chunk table with a halving tail: full chunks while more than two remain, then halves down
+    // to chunk_min samples, so the launch ends on short units (results do not depend on chunking)
+    c->P.nct = 0;
+    if (c->chunk_min > 0 && c->chunk_min < c->P.chunk) {
+        int rem = s1 - s0, n = 0, at = 0;
+        c->P.cbeg[0] = 0;
+        while (rem > 0 && n < JT_MAX_CHUNKS) {
+            int k = rem > 2 * c->P.chunk ? c->P.chunk : std::max(c->chunk_min, (rem + 1) / 2);
+            k = std::min(k, rem);
+            at += k;
+            rem -= k;
+            c->P.cbeg[++n] = at;
+        }
+        if (rem == 0) c->P.nct = n;
+    }
     (void)hipSetDevice(c->device);
     hipError_t e = hipMemsetAsync(c->A.work, 0, (size_t)(c->tiles + NBANDS * BAND_STRIDE) * 4, c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
@@ -3175,10 +3210,10 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     char tmp[512];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d light_lanes=%d chunk=%d tiles=%d block=%d wf_groups=%d env_alias=%d",
+                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d wf_groups=%d env_alias=%d",
                   c->P.wf_groups ? "trace_kernel_wf" : c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, c->kmask, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
-                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->tiles, BLOCK, c->P.wf_groups,
+                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->P.nct, c->tiles, BLOCK, c->P.wf_groups,
                   c->env_alias ? 1 : 0);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;

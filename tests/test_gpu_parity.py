@@ -226,11 +226,19 @@ def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sa
     lights = trace.make_trace_lights(cornell_abi, lib)
     p = make_params(abi, resolution=72, samples=9, sampler=sampler)
     outs = []
-    for chunk in ("1000", "1", "4"):
+    # uniform chunks of 1000 (one per tile), 1 and 4 samples; then chunk tables ending in a
+    # halving tail (JT_CHUNK_MIN): 4,3,1,1 and 2,2,2,2,1
+    for chunk, cmin in (("1000", None), ("1", None), ("4", None), ("4", "1"), ("2", "1")):
         monkeypatch.setenv("JT_CHUNK", chunk)
+        if cmin is None:
+            monkeypatch.delenv("JT_CHUNK_MIN", raising=False)
+        else:
+            monkeypatch.setenv("JT_CHUNK_MIN", cmin)
         st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
         st.trace_range(0, 9)
         outs.append((st.get_image(), st.get_aovs(), st.counters()))
+        desc = st.describe()
+        assert ("chunk_table=0" in desc) == (cmin is None), desc
         st.close()
     for o in outs[1:]:
         assert np.array_equal(outs[0][0], o[0])
