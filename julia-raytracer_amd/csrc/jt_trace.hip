@@ -2014,7 +2014,8 @@ struct jt_ctx {
     int total_samples = 0, batch = 1, sampler = 1;
     int cus = 256;   // compute units of the device (persistent grid size)
     int chunk = 0;   // samples per work unit (0: chosen per launch)
-    int chunk_min = 0;  // > 0: the launch's chunk table ends with a halving tail down to this many samples
+    int chunk_min = -1;  // > 0: the launch's chunk table ends with a halving tail down to this many
+                         // samples; 0: uniform chunks; -1: auto (LDS mode: half a chunk)
     int tiles = 0;   // 8x8 pixel tiles
     int stack = 16;  // stack bound of the scene (entries); > 16: LDS ring of `ring` + HBM overflow
     int ring = 16;
@@ -2916,12 +2917,17 @@ int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
     c->P.chunk = c->chunk > 0 ? c->chunk : std::max(8, std::min(64, (s1 - s0) / 4));
     // chunk table with a halving tail: full chunks while more than two remain, then halves down
     // to chunk_min samples, so the launch ends on short units (results do not depend on chunking)
+    // Auto: LDS-mode (small-scene) launches of >= 32-sample chunks end on half chunks: +1.2 % on
+    // cornellbox 256 spp, +0.7 % at 128 spp (32 spp: within noise); HBM-mode scenes gain nothing
+    // (bathroom1 even, features2 -2 %)
+    // (profiles/r02_chunk_tail.txt)
+    const int cmin = c->chunk_min >= 0 ? c->chunk_min : (c->lds_scene_bytes > 0 && c->P.chunk >= 32 ? c->P.chunk / 2 : 0);
     c->P.nct = 0;
-    if (c->chunk_min > 0 && c->chunk_min < c->P.chunk) {
+    if (cmin > 0 && cmin < c->P.chunk) {
         int rem = s1 - s0, n = 0, at = 0;
         c->P.cbeg[0] = 0;
         while (rem > 0 && n < JT_MAX_CHUNKS) {
-            int k = rem > 2 * c->P.chunk ? c->P.chunk : std::max(c->chunk_min, (rem + 1) / 2);
+            int k = rem > 2 * c->P.chunk ? c->P.chunk : std::max(cmin, (rem + 1) / 2);
             k = std::min(k, rem);
             at += k;
             rem -= k;

@@ -226,9 +226,9 @@ def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sa
     lights = trace.make_trace_lights(cornell_abi, lib)
     p = make_params(abi, resolution=72, samples=9, sampler=sampler)
     outs = []
-    # uniform chunks of 1000 (one per tile), 1 and 4 samples; then chunk tables ending in a
-    # halving tail (JT_CHUNK_MIN): 4,3,1,1 and 2,2,2,2,1
-    for chunk, cmin in (("1000", None), ("1", None), ("4", None), ("4", "1"), ("2", "1")):
+    # uniform chunks of 1000 (one per tile), 1 and 4 samples (JT_CHUNK_MIN=0); chunk tables
+    # ending in a halving tail: 4,3,1,1 and 2,2,2,2,1; the auto tail of 64-sample chunks (9 samples: one chunk)
+    for chunk, cmin in (("1000", "0"), ("1", "0"), ("4", "0"), ("4", "1"), ("2", "1"), ("64", None)):
         monkeypatch.setenv("JT_CHUNK", chunk)
         if cmin is None:
             monkeypatch.delenv("JT_CHUNK_MIN", raising=False)
@@ -238,7 +238,7 @@ def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sa
         st.trace_range(0, 9)
         outs.append((st.get_image(), st.get_aovs(), st.counters()))
         desc = st.describe()
-        assert ("chunk_table=0" in desc) == (cmin is None), desc
+        assert ("chunk_table=0" in desc) == (cmin == "0"), desc
         st.close()
     for o in outs[1:]:
         assert np.array_equal(outs[0][0], o[0])
