@@ -993,6 +993,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #if JT_STAMPS
     unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
     unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
+    unsigned long long dead_lanes = 0;  // lanes done with their unit's samples, per traversal iteration
 #endif
     const int tiles_x = (P.width + 7) / 8, tiles = tiles_x * ((P.height + 7) / 8);
     const int nchunks = num_chunks(P, s_begin, s_end);
@@ -1097,6 +1098,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
 #if JT_STAMPS
             n_trav++;
+            dead_lanes += 64 - lane_count(__builtin_amdgcn_ballot_w64(T.sp >= 0));
             if (np >= nn) { steps_p++; lanes_p += np; } else { steps_n++; lanes_n += nn; }
 #endif
             if (np >= nn) {
@@ -1241,6 +1243,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         atomicAdd(dbg + 12, n_lhit);
         atomicAdd(dbg + 13, n_phit);
         atomicAdd(dbg + 14, n_fin);
+        atomicAdd(dbg + 15, dead_lanes);
     }
 #endif
     // one atomic per counter per wave

@@ -23,7 +23,7 @@ st.set_counters(0)
 st.trace_range(0, spp)
 v = (C.c_ulonglong * 16)()
 abi.check(lib, lib.jt_debug_stamps(st.handle, v))
-t_trav, t_shade, n_trav, n_shade, lanes_p, lanes_n, steps_p, steps_n, t_lhit, t_phit, t_fin, t_qb, n_lhit, n_phit, n_fin, _ = list(v)
+t_trav, t_shade, n_trav, n_shade, lanes_p, lanes_n, steps_p, steps_n, t_lhit, t_phit, t_fin, t_qb, n_lhit, n_phit, n_fin, dead = list(v)
 tot = t_trav + t_shade
 print(f"wait_lanes={os.environ.get('JT_WAIT_LANES', 'default')} spp={spp} kernel_ms={st.counters()['kernel_ms']:.1f}")
 print(f"traversal phase {t_trav / tot:.1%}  shading phase {t_shade / tot:.1%}")
@@ -34,3 +34,4 @@ print(f"prim steps {steps_p} (avg lanes {lanes_p / max(1, steps_p):.1f}), node s
 print(f"shading split: light_hit {t_lhit / t_shade:.1%} ({t_lhit / max(1, n_lhit):.0f} cyc x {n_lhit}), "
       f"path_hit {t_phit / t_shade:.1%} ({t_phit / max(1, n_phit):.0f} cyc x {n_phit}), "
       f"finish+restart {t_fin / t_shade:.1%} (phases with a finished sample {n_fin}), query_begin {t_qb / t_shade:.1%}")
+print(f"lanes already done with their work unit, per traversal iteration: {dead / max(1, n_trav):.1f} of 64")
