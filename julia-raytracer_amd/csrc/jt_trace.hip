@@ -47,6 +47,12 @@
 #ifndef JT_CHILD_PRETEST
 #define JT_CHILD_PRETEST 1
 #endif
+// HBM mode: read the TLAS top from the workgroup's LDS copy. Off: the LDS-or-global choice made
+// the compiler emit flat node loads, which cost more than the cache saved (global loads:
+// features2 +2.7 %, bathroom1 +1.1 %, ecosys +3.2 %; gpurun_out/ab_notl)
+#ifndef JT_TLAS_LDS
+#define JT_TLAS_LDS 0
+#endif
 
 using namespace jtd;
 
@@ -427,11 +433,17 @@ template <int RING, bool OVF>
 __device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* stack, int pixel) {
     T.sp -= 1;
     if (OVF) {
+        // the ring slot is read unconditionally (its address is always valid; a relaxed atomic
+        // load, which the compiler cannot merge with the HBM load) and the HBM entry only below
+        // the ring: written as a choice of the two addresses, the compiler made every pop one
+        // flat load waiting on both memory counters
+        const unsigned r = (unsigned)__hip_atomic_load(stack + (T.sp & (S.ring - 1)) * BLOCK, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
         if (T.sp < T.low) {  // below the ring: this entry was spilled
             T.low = T.sp;
             return (unsigned)S.ovf[(size_t)pixel * S.ovf_stride + T.sp];
         }
-        return (unsigned)stack[(T.sp & (S.ring - 1)) * BLOCK];
+        return r;
     }
     return (unsigned)stack[T.sp * BLOCK];
 }
@@ -481,12 +493,12 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         } else if (JT_POP_LDS) {
             const uint4 pc = S.pcl[threadIdx.x];
             if (pc.x == idx) nb = make_float4(0.0f, 0.0f, __uint_as_float(pc.y), __uint_as_float(pc.z));
-            else nb = ((int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
+            else nb = (JT_TLAS_LDS && (int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
         } else {
-            nb = ((int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
+            nb = (JT_TLAS_LDS && (int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
         }
     } else {
-        const DNode nd = (NCACHE && (int)idx < S.nlnodes) ? S.lnodes[idx] : S.nodes[idx];
+        const DNode nd = (NCACHE && JT_TLAS_LDS && (int)idx < S.nlnodes) ? S.lnodes[idx] : S.nodes[idx];
         if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
         nb = nd.b;
     }
@@ -504,7 +516,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             // only shrinks): count its pop and skip the push. A pushed child is tested again when
             // popped, with that moment's tmax, exactly as the reference does. (+10 % bathroom1,
             // +14 % ecosys; in LDS mode the extra tests cost more than the pops they save.)
-            const bool cached = (int)c_near < S.nlnodes && (int)c_far < S.nlnodes;
+            const bool cached = JT_TLAS_LDS && (int)c_near < S.nlnodes && (int)c_far < S.nlnodes;
             const DNode n0 = cached ? S.lnodes[c_far] : S.nodes[c_far];
             const DNode n1 = cached ? S.lnodes[c_near] : S.nodes[c_near];
             const bool k0 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n0.a, n0.b);
@@ -2695,7 +2707,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         // per CU (160 KiB / 4 minus the stack ring and the running means); JT_NODE_CACHE caps it
         S.lnodes = nullptr;
         S.nlnodes = 0;
-        if (!S.blob_n16) {
+        if (!S.blob_n16 && JT_TLAS_LDS) {
             const long left = (long)(lds_cu / 4) - (long)base_bytes;
             long n = std::min<long>((long)tlas.size(), std::max<long>(0, left) / (long)sizeof(DNode));
             if (const char* v = std::getenv("JT_NODE_CACHE")) n = std::min<long>(n, std::max(0, std::atoi(v)));

@@ -171,8 +171,9 @@ def test_feature_specialisation_bitwise_equal(gpu, abi, lib, cornell_abi, sample
 
 @pytest.mark.parametrize("sampler", [1, 2])
 def test_tlas_node_cache_is_bitwise_invariant(gpu, abi, lib, cornell_abi, sampler, monkeypatch):
-    """HBM mode reads the breadth-first top of the TLAS from an LDS copy: none, part or all of
-    it cached gives the same bits (the node order in memory is storage only)."""
+    """HBM mode can read the breadth-first top of the TLAS from an LDS copy (built with
+    JT_TLAS_LDS=1; the default build compiles the cache out): none, part or all of it
+    cached gives the same bits (the node order in memory is storage only)."""
     from jtrace import trace
     bvh = trace.make_scene_bvh(cornell_abi, False, lib)
     lights = trace.make_trace_lights(cornell_abi, lib)
