@@ -50,6 +50,9 @@
 // HBM mode: read the TLAS top from the workgroup's LDS copy. Off: the LDS-or-global choice made
 // the compiler emit flat node loads, which cost more than the cache saved (global loads:
 // features2 +2.7 %, bathroom1 +1.1 %, ecosys +3.2 %; gpurun_out/ab_notl)
+#ifndef JT_RAY_FROM_PATH
+#define JT_RAY_FROM_PATH 1
+#endif
 #ifndef JT_TLAS_LDS
 #define JT_TLAS_LDS 0
 #endif
@@ -614,14 +617,15 @@ enum : int { PH_SCENE = 0, PH_LIGHT = 1, PH_FINISH = 2 };  // PH_FINISH: path do
 enum : int { F_HIT = 1, F_VOLUME = 2 };
 
 struct Path {
-    v3 o, d;                    // pending ray; during PH_LIGHT: shading position / incoming
+    v3 o, d;                    // pending ray (during PH_LIGHT the light query's: origin / incoming)
     v3 radiance, weight;  // during PH_LIGHT weight already holds weight .* f (src/trace.jl:386)
     Rng rng;
     int bounce, opbounce, flags, phase;
     float max_roughness;
     // sample_lights_pdf in flight (src/trace.jl:1010-1084)
     int li, lcount;
-    v3 lq;       // next_position of the current instance light
+    v3 lq;       // during PH_LIGHT: the shading position (st.o holds the light query's origin,
+                 // next_position of src/trace.jl:1039, so every query's ray is (st.o, st.d))
     float pb;    // sample_bsdfcos_pdf / sample_scattering_pdf
     float pdf, lpdf;
     Volume vol;  // volume_stack[1] (the stack never holds more than one entry)
@@ -651,6 +655,7 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
     for (;;) {
         st.li += 1;
         if (st.li >= S.nlights) {
+            st.o = st.lq;  // the next bounce's ray starts at the shading position
             const float pdf = st.pdf * sample_uniform_pdf(S.nlights);
             st.weight = st.weight / (0.5f * st.pb + 0.5f * pdf);  // (weight .* f) / (...)
             return after_weight(P, st);
@@ -659,7 +664,7 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
         if (l.instance >= 0) {
             st.lpdf = 0.0f;
             st.lcount = 0;
-            st.lq = st.o;
+            st.o = st.lq;  // the first query starts at the shading position
             st.phase = PH_LIGHT;
             return false;
         }
@@ -670,6 +675,7 @@ template <int F>
 __device__ __forceinline__ bool begin_light_pdf(const DScene& S, const DParams& P, Path& st) {
     st.pdf = 0.0f;
     st.li = -1;
+    st.lq = st.o;
     return light_advance<F>(S, P, st);
 }
 // one intersect_instance_bvh result of the instance-light loop (src/trace.jl:1024-1044)
@@ -680,9 +686,9 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
         v3 lposition = eval_position<F>(S, l.instance, h.elem, V2(h.u, h.v));
         v3 lnormal = eval_element_normal(S, l.instance, h.elem);
         const float area = S.cdf[l.cdf_offset + l.ncdf - 1];
-        v3 dd = lposition - st.o;
+        v3 dd = lposition - st.lq;
         st.lpdf += dot(dd, dd) / (__builtin_fabsf(dot(lnormal, st.d)) * area);
-        st.lq = lposition + st.d * 0.001f;
+        st.o = lposition + st.d * 0.001f;
         if (++st.lcount < 100) return false;
     }
     st.pdf += st.lpdf;
@@ -704,15 +710,30 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
 #ifndef JT_ACC_HBM
 #define JT_ACC_HBM 0
 #endif
-// Not in the FT_NONE kernels: cornellbox's LDS-mode kernel then no longer fits 5 workgroups per
-// CU (-9 %); the mesh kernels gain (features2 +7 %, bathroom1 +1 %, ecosys +0.6 %).
-__host__ __device__ constexpr bool lane_lds(int F) { return JT_LANE_LDS && F != FT_NONE; }
+// The mesh kernels gain (features2 +7 %, bathroom1 +1 %, ecosys +0.6 %). The FT_NONE kernels
+// keep only the sample index (12 slots, the weight is recomputed from it): with 13 slots
+// cornellbox's LDS-mode kernel no longer fit 5 workgroups per CU (-9 %); with 12 it does, and
+// its spills drop from 37 to 23 VGPRs (scratch 112 -> 80 B/lane, spill write-back 36.3 -> 22.6
+// GB per launch, +0.5 %; gpurun_out/ab_ll, s8).
+#ifndef JT_LANE_LDS_NONE
+#define JT_LANE_LDS_NONE 1
+#endif
+__host__ __device__ constexpr bool lane_lds(int F) { return JT_LANE_LDS && (F != FT_NONE || JT_LANE_LDS_NONE); }
 constexpr int ACC_SLOTS = JT_LANE_LDS ? 13 : 11;  // the host sizes LDS for the larger layout
+// Lane-LDS slots: [11] the lane's sample index, [12] its running-mean weight. The FT_NONE
+// kernels (JT_LANE_LDS_NONE) recompute the weight from the sample index instead of storing it:
+// with 12 slots cornellbox's LDS-mode workgroup still fits 5 per CU.
+__host__ __device__ constexpr int acc_slots(int F) { return lane_lds(F) ? (F == FT_NONE ? 12 : 13) : 11; }
 struct Aov {
     float* acc;
-    float w_;  // !lane_lds(F)
+    float w_;    // !lane_lds(F)
+    int first_;  // params.first (the weight's sample offset)
     template <int F>
-    __device__ __forceinline__ float w() const { return lane_lds(F) ? acc[12 * BLOCK] : w_; }
+    __device__ __forceinline__ float w() const {
+        if (!lane_lds(F)) return w_;
+        if (F == FT_NONE) return 1.0f / (float)(reinterpret_cast<const int*>(acc)[11 * BLOCK] - first_ + 1);
+        return acc[12 * BLOCK];
+    }
 };
 template <int F>
 __device__ __forceinline__ void aov_update(const Aov& a, v3 ta, v3 tn) {
@@ -1000,7 +1021,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     // JT_ACC_HBM (experiment, FT_NONE kernels): the running-mean slots in a per-lane HBM (L2)
     // area instead of LDS, so more workgroups fit per CU
     constexpr bool AH = JT_ACC_HBM && !LL;
-    __shared__ float acc_lds[AH ? 1 : (LL ? 13 : 11) * BLOCK];
+    __shared__ float acc_lds[AH ? 1 : acc_slots(F) * BLOCK];
     float* acc = AH ? reinterpret_cast<float*>(A.pool) + (size_t)blockIdx.x * 11 * BLOCK + threadIdx.x : acc_lds + threadIdx.x;
 #if JT_STAMPS
     unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
@@ -1047,11 +1068,11 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         reinterpret_cast<int*>(acc)[10 * BLOCK] = 0;
     }
     int* const acc_i = reinterpret_cast<int*>(acc);
-    Aov aov{acc, 0.0f};
+    Aov aov{acc, 0.0f, P.first};
     if (LL) {
         if (in_image) {
             acc_i[11 * BLOCK] = sample;
-            acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+            if (F != FT_NONE) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
         }
     } else {
         aov.w_ = 1.0f / (float)(sample - P.first + 1);
@@ -1097,7 +1118,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                             st.phase = PH_FINISH;
                         } else if (st.phase == PH_LIGHT) {
                             cnt.light_queries++;
-                            query_begin(T, st.lq, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
+                            query_begin(T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
                         } else {
                             cnt.rays++;
                             query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
@@ -1113,6 +1134,13 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             dead_lanes += 64 - lane_count(__builtin_amdgcn_ballot_w64(T.sp >= 0));
             if (np >= nn) { steps_p++; lanes_p += np; } else { steps_n++; lanes_n += nn; }
 #endif
+            if (JT_RAY_FROM_PATH && !(F & FT_XFORM)) {
+                // without instance transforms a query's ray is its path's (st.o, st.d), unchanged
+                // while the query runs: re-reading it here keeps one copy, not two, live across
+                // the loop (register renaming only, no instructions)
+                T.lo = st.o;
+                T.ld = st.d;
+            }
             if (np >= nn) {
                 if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
             } else {
@@ -1181,7 +1209,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                     T.sp = -1;
                 } else {
                     acc_i[11 * BLOCK] = sample;
-                    acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+                    if (F != FT_NONE) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
                     const int lx = opaque_lane_id();
                     const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
                     start_path(P, i2, j2, j2 * P.width + i2, sample, st);
@@ -1203,7 +1231,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (alive) {
                 if (SAMPLER == 1 && st.phase == PH_LIGHT) {
                     cnt.light_queries++;
-                    query_begin(T, st.lq, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
+                    query_begin(T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
                 } else {
                     cnt.rays++;
                     query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
@@ -1496,7 +1524,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
     // a slot's pending query (LDS): origin, direction, root
     auto issue = [&](int s, const Path& st) {
         const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
-        const v3 o = light ? st.lq : st.o;
+        const v3 o = st.o;
         const unsigned root = light ? (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance
                                     : (T_TLAS << 30) | SNAP_NONE;
         q_o[s] = make_float4(o.x, o.y, o.z, __uint_as_float(root));
@@ -1724,7 +1752,7 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
             // sample_lights_pdf's instance queries, inline (src/trace.jl:1018-1044)
             while (SAMPLER == 1 && !done && st.phase == PH_LIGHT) {
                 cnt.light_queries++;
-                query_begin(T, st.lq, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
+                query_begin(T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
                 while (T.sp > 0 || T.nprim > 0) {
                     if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
                     else node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
