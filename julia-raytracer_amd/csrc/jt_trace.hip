@@ -1017,6 +1017,12 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                                            int* stack) {
     const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    // WC: paths, scene rays and light queries are counted per wave (ballots at wave-uniform
+    // points, scalar registers), not per lane: three fewer VGPRs live across the traversal loop.
+    // The mesh kernels gain (bathroom1 +3 %, features2 +1 %); the FT_NONE kernel, whose light-hit
+    // steps run the ballots every few iterations, loses 1.5 % and keeps per-lane counters.
+    constexpr bool WC = F != FT_NONE;
+    unsigned w_paths = 0, w_rays = 0, w_lq = 0;
     constexpr bool LL = lane_lds(F);
     // JT_ACC_HBM (experiment, FT_NONE kernels): the running-mean slots in a per-lane HBM (L2)
     // area instead of LDS, so more workgroups fit per CU
@@ -1085,9 +1091,10 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     T.nprim = 0;
     if (alive) {
         start_path(P, i, j, pixel, sample, st);
-        cnt.rays++;
         query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
     }
+    if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(alive));
+    else cnt.rays += alive ? 1 : 0;
     for (;;) {
 #if JT_STAMPS
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -1113,16 +1120,23 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 const bool wantl = waiting && st.phase == PH_LIGHT;
                 const int nl = lane_count(__builtin_amdgcn_ballot_w64(wantl));
                 if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
+                    bool c_lq = false, c_ray = false;
                     if (wantl) {
                         if (light_hit<F>(S, P, st, query_hit(T))) {
                             st.phase = PH_FINISH;
                         } else if (st.phase == PH_LIGHT) {
-                            cnt.light_queries++;
+                            if (WC) c_lq = true;
+                            else cnt.light_queries++;
                             query_begin(T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
                         } else {
-                            cnt.rays++;
+                            if (WC) c_ray = true;
+                            else cnt.rays++;
                             query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
                         }
+                    }
+                    if (WC) {
+                        w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
+                        w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
                     }
                     continue;
                 }
@@ -1158,6 +1172,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         n_shade++;
 #endif
         // shading phase: every waiting lane consumes its hit and issues its next query
+        bool c_path = false, c_lq = false, c_ray = false;
         if ((T.sp | T.nprim) == 0) {
             bool alive = true;
             const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
@@ -1183,7 +1198,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
             if (done) {
                 // trace_sample epilogue (src/trace.jl:625-648)
-                cnt.paths++;
+                if (WC) c_path = true;
+                else cnt.paths++;
                 v3 radiance = st.radiance;
                 if (!all_finite(radiance)) radiance = V3(0, 0, 0);
                 const float mr = max3(radiance);
@@ -1230,10 +1246,12 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
             if (alive) {
                 if (SAMPLER == 1 && st.phase == PH_LIGHT) {
-                    cnt.light_queries++;
+                    if (WC) c_lq = true;
+                    else cnt.light_queries++;
                     query_begin(T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
                 } else {
-                    cnt.rays++;
+                    if (WC) c_ray = true;
+                    else cnt.rays++;
                     query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
                 }
                 // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
@@ -1249,6 +1267,11 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #if JT_STAMPS
         t_shade += __builtin_amdgcn_s_memtime() - t1;
 #endif
+        if (WC) {
+            w_paths += lane_count(__builtin_amdgcn_ballot_w64(c_path));
+            w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
+            w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
+        }
         if (__ballot(T.sp >= 0) == 0) break;
     }
     if constexpr (LL) {
@@ -1287,11 +1310,12 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     }
 #endif
     // one atomic per counter per wave
+    const unsigned wv[3] = {w_paths, w_rays, w_lq};
     unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
                      COUNT ? cnt.shades : 0u};
 #pragma unroll
     for (int k = 0; k < 7; k++) {
-        unsigned s = wave_sum(v[k]);
+        unsigned s = (WC && k < 3) ? wv[k] : wave_sum(v[k]);
         if (lane == 0 && s) atomicAdd(&A.counters[k], (unsigned long long)s);
     }
 }
