@@ -93,8 +93,8 @@ def cpu_baseline(scene_abi, params, width, height, nthreads, spp=2):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)  # ~1.8 s of GPU work at N=1
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--spp", type=int, default=256)

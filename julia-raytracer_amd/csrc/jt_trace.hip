@@ -32,6 +32,11 @@
 #ifndef JT_STAMPS
 #define JT_STAMPS 0
 #endif
+// pops per node iteration: the LDS-mode FT_NONE kernel (cornellbox) gains with 4 (+1.2 %),
+// the HBM-mode mesh kernels lose with 4 or 2 (bathroom1 -4 %, ecosys -1.5 %; gpurun_out/ab_nr)
+#ifndef JT_NODE_REPEAT_NONE
+#define JT_NODE_REPEAT_NONE 4
+#endif
 #ifndef JT_NODE_REPEAT
 #define JT_NODE_REPEAT 3
 #endif
@@ -1161,8 +1166,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 // JT_NODE_REPEAT pops per node iteration: a lane whose next step is again a
                 // stack pop takes it at once (the same steps in the same per-lane order, less
                 // per-iteration vote and loop overhead)
+                constexpr int NREP = F == FT_NONE ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
 #pragma unroll
-                for (int k = 0; k < JT_NODE_REPEAT; k++)
+                for (int k = 0; k < NREP; k++)
                     if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
             }
         }
