@@ -11,9 +11,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#ifndef JT_SLAB_FAST
-#define JT_SLAB_FAST 0
-#endif
 #ifndef JT_MAX_CHUNKS
 #define JT_MAX_CHUNKS 32
 #endif
@@ -132,13 +129,6 @@ struct DScene {
     // units; -1 = not in the blob). Texels, environments and LUTs stay in HBM.
     const uint4* blob;
     int blob_n16;
-    // HBM mode: nodes [0, nlnodes) — the top of the TLAS, laid out breadth-first — are copied
-    // into LDS by every workgroup and read from there (lnodes)
-    const DNode* lnodes;
-    int nlnodes;
-    // HBM mode, JT_POP_LDS: one LDS record per lane (node index, start, meta) of the child the
-    // last pre-test pushed (set by the kernel; nullptr elsewhere)
-    uint4* pcl;
     // traversal-stack overflow (scenes deeper than the LDS ring): ovf_stride entries per pixel
     int* ovf;
     int ovf_stride;
@@ -171,9 +161,6 @@ struct DParams {
     // full chunks, then a halving tail that shortens the launch's last units (JT_CHUNK_MIN)
     int nct;
     int cbeg[JT_MAX_CHUNKS + 1];
-    int wf_groups;  // WF body: 64-slot path groups per workgroup
-    int wf_refill;  // WF body: idle lanes that make a traversal step first take new queries
-    int wf_shaders; // WF body: shading waves per workgroup (the others traverse)
     unsigned long long seed;
 };
 
@@ -514,25 +501,10 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
 }
 
 // The slab test's final compare, `t1 *= 1.00000024; t0 <= t1` (src/geometry.jl:102-103): the
-// Float32 t1 is promoted, so the product and the compare are Float64.
-__device__ __forceinline__ bool slab_pass(float t0, float t1) {
-#if JT_SLAB_FAST
-    // Decided in float where that is exact; callers guarantee t0 >= tmin > 0 (t0 is a max with
-    // ray_eps) for non-NaN slabs. t0 <= t1 implies t0 <= t1*c (c > 1, t1 > 0). t0 > RN_f(t1 * k),
-    // k = 1 + 5*2^-23, implies t0 > RN_d(t1*c), since k(1 - 2^-24) > c(1 + 2^-53) for t1 > 0 (a
-    // denormal, zero or negative t1 is below tmin either way). Only t1 < t0 <= RN_f(t1 k), a few
-    // ulps, takes the double compare, behind a wave-uniform branch.
-    // scripts/exhaustive/slab_check.hip checks this against the double compare for every t1.
-    bool pass = t0 <= t1;
-    const bool amb = !pass && t0 <= t1 * 1.0000006f;
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(amb) != 0, 0)) {
-        if (amb) pass = (double)t0 <= (double)t1 * 1.00000024;
-    }
-    return pass;
-#else
-    return (double)t0 <= (double)t1 * 1.00000024;
-#endif
-}
+// Float32 t1 is promoted, so the product and the compare are Float64. (An exact float decision
+// with a double fallback — checked exhaustively, scripts/exhaustive/slab_check.hip — measured
+// slower on gfx950, whose wave64 FP64 multiply issues at the FP32 rate)
+__device__ __forceinline__ bool slab_pass(float t0, float t1) { return (double)t0 <= (double)t1 * 1.00000024; }
 
 // intersect_bbox (src/geometry.jl:96-105): Julia min/max; `t1 *= 1.00000024` is Float64.
 // Any NaN slab value makes Julia's t0 or t1 NaN and culls the box; that case is tested

@@ -43,23 +43,11 @@
 #ifndef JT_FIRST_POP
 #define JT_FIRST_POP 1
 #endif
-#ifndef JT_POP_CACHE
-#define JT_POP_CACHE 0
-#endif
-#ifndef JT_POP_LDS
-#define JT_POP_LDS 0
-#endif
 #ifndef JT_CHILD_PRETEST
 #define JT_CHILD_PRETEST 1
 #endif
-// HBM mode: read the TLAS top from the workgroup's LDS copy. Off: the LDS-or-global choice made
-// the compiler emit flat node loads, which cost more than the cache saved (global loads:
-// features2 +2.7 %, bathroom1 +1.1 %, ecosys +3.2 %; gpurun_out/ab_notl)
 #ifndef JT_RAY_FROM_PATH
 #define JT_RAY_FROM_PATH 1
-#endif
-#ifndef JT_TLAS_LDS
-#define JT_TLAS_LDS 0
 #endif
 
 using namespace jtd;
@@ -314,11 +302,6 @@ struct Trav {
     int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
     float h_u, h_v;
     int nh;              // hits accepted so far (every tmax change), saturating at 63
-    // JT_POP_CACHE (HBM mode): start/meta words of the child the last pre-test pushed — the
-    // next pop when the lane's next step is a pop — so that pop loads nothing (node records
-    // are immutable: a cached index always maps to its own words)
-    unsigned pc_idx;
-    float pc_start, pc_meta;
 };
 
 __device__ __forceinline__ int neg_mask(v3 d) { return (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0); }
@@ -359,7 +342,6 @@ __device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, 
     stack[0] = (int)root;
     T.sp = 1;
     T.low = 0;
-    T.pc_idx = ~0u;
 }
 
 // The current BLAS leaf's next primitive(s), in order (src/bvh.jl:444-484). Triangles go in
@@ -496,17 +478,9 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
     const unsigned snap = (e >> 24) & 63u;
     float4 nb;
     if (NCACHE && snap != 63u && snap == (unsigned)T.nh) {
-        if (JT_POP_CACHE && idx == T.pc_idx) {
-            nb = make_float4(0.0f, 0.0f, T.pc_start, T.pc_meta);  // z, w only
-        } else if (JT_POP_LDS) {
-            const uint4 pc = S.pcl[threadIdx.x];
-            if (pc.x == idx) nb = make_float4(0.0f, 0.0f, __uint_as_float(pc.y), __uint_as_float(pc.z));
-            else nb = (JT_TLAS_LDS && (int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
-        } else {
-            nb = (JT_TLAS_LDS && (int)idx < S.nlnodes) ? S.lnodes[idx].b : S.nodes[idx].b;
-        }
+        nb = S.nodes[idx].b;
     } else {
-        const DNode nd = (NCACHE && JT_TLAS_LDS && (int)idx < S.nlnodes) ? S.lnodes[idx] : S.nodes[idx];
+        const DNode nd = S.nodes[idx];
         if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
         nb = nd.b;
     }
@@ -524,23 +498,14 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             // only shrinks): count its pop and skip the push. A pushed child is tested again when
             // popped, with that moment's tmax, exactly as the reference does. (+10 % bathroom1,
             // +14 % ecosys; in LDS mode the extra tests cost more than the pops they save.)
-            const bool cached = JT_TLAS_LDS && (int)c_near < S.nlnodes && (int)c_far < S.nlnodes;
-            const DNode n0 = cached ? S.lnodes[c_far] : S.nodes[c_far];
-            const DNode n1 = cached ? S.lnodes[c_near] : S.nodes[c_near];
+            const DNode n0 = S.nodes[c_far];
+            const DNode n1 = S.nodes[c_near];
             const bool k0 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n0.a, n0.b);
             const bool k1 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n1.a, n1.b);
             if (COUNT) cnt.nodes += (k0 ? 0 : 1) + (k1 ? 0 : 1);
             const unsigned ptag = type << 30 | (unsigned)T.nh << 24;  // pre-tested at hit count nh
             if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_far);
             if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_near);
-            if (JT_POP_LDS && (k0 || k1))
-                S.pcl[threadIdx.x] = make_uint4(k1 ? c_near : c_far, __float_as_uint(k1 ? n1.b.z : n0.b.z),
-                                                __float_as_uint(k1 ? n1.b.w : n0.b.w), 0u);
-            if (JT_POP_CACHE) {  // the child pushed last is popped next if this lane pops next
-                T.pc_idx = k1 ? c_near : (k0 ? c_far : T.pc_idx);
-                T.pc_start = k1 ? n1.b.z : (k0 ? n0.b.z : T.pc_start);
-                T.pc_meta = k1 ? n1.b.w : (k0 ? n0.b.w : T.pc_meta);
-            }
         } else {
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_far);
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_near);
@@ -711,9 +676,6 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
 // state parked in LDS instead of registers kept live (and spilled) across the traversal loop.
 #ifndef JT_LANE_LDS
 #define JT_LANE_LDS 1
-#endif
-#ifndef JT_ACC_HBM
-#define JT_ACC_HBM 0
 #endif
 // The mesh kernels gain (features2 +7 %, bathroom1 +1 %, ecosys +0.6 %). The FT_NONE kernels
 // keep only the sample index (12 slots, the weight is recomputed from it): with 13 slots
@@ -964,8 +926,6 @@ struct DAccum {
     unsigned* work;                // unit counters of the launch, one per XCD band at work[16 b]
                                    // (zeroed before each launch)
     int* tile_done;                // per 8x8 tile: sample chunks accumulated in this launch
-    float4* pool;                  // WF body: path-slot records (HBM), pool_bytes long
-    size_t pool_bytes;
 };
 
 // Work units: (sample chunk c, 8x8 pixel tile t), fetched by whole waves from atomic counters,
@@ -1029,11 +989,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     constexpr bool WC = F != FT_NONE;
     unsigned w_paths = 0, w_rays = 0, w_lq = 0;
     constexpr bool LL = lane_lds(F);
-    // JT_ACC_HBM (experiment, FT_NONE kernels): the running-mean slots in a per-lane HBM (L2)
-    // area instead of LDS, so more workgroups fit per CU
-    constexpr bool AH = JT_ACC_HBM && !LL;
-    __shared__ float acc_lds[AH ? 1 : acc_slots(F) * BLOCK];
-    float* acc = AH ? reinterpret_cast<float*>(A.pool) + (size_t)blockIdx.x * 11 * BLOCK + threadIdx.x : acc_lds + threadIdx.x;
+    __shared__ float acc_lds[acc_slots(F) * BLOCK];
+    float* acc = acc_lds + threadIdx.x;
 #if JT_STAMPS
     unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
     unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
@@ -1326,541 +1283,6 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     }
 }
 
-// ============================================================================ WF body
-// trace_samples with the queries decoupled from the paths (DESIGN.md §2 "WF scheduling"). A
-// workgroup owns NP = 64 * G path slots: G slot groups, each one 8x8 tile x sample chunk (more
-// paths than its 256 lanes). Between shading steps a slot's path state and its pixel's running
-// means live in a record in HBM (L2); its pending BVH query (origin, direction, root) in LDS.
-// Three LDS rings hold slot ids: queries waiting for a lane, scene results and light results
-// waiting for shading. Each wave repeatedly picks one wave-uniform job:
-//   - start a slot group on a new work unit (64 new paths, one per lane);
-//   - shade a batch of up to 64 waiting results (scene or light ring): load the slot record,
-//     path_hit / naive_hit / light_hit, then issue the slot's next query or finish its sample;
-//   - traverse for a few iterations: lanes without a query take one from the ring, then one
-//     node/primitive step kind (the megakernel's step code).
-// A query runs on one lane to completion (its stack is that lane's LDS stack), but any lane may
-// run any slot's query and any wave may shade any slot: traversal runs on nearly full waves and
-// shading on full batches. Each path's float operations and RNG draws are the reference's, in
-// its order, and a pixel's samples are accumulated in order (one slot per pixel and chunk; the
-// chunks of a tile in order): results are bit-identical to trace_body.
-constexpr int WF_GMAX = 8;
-constexpr int WF_TRAV = 0, WF_SCENE = 1, WF_LIGHT = 2;
-struct WfCtl {
-    unsigned head[3], tail[3];  // ring cursors
-    unsigned attn;              // groups a wave should look at: idle while units remain, or waiting on a tile
-    unsigned live;              // groups holding (or claiming) a unit
-    int g_tile[WF_GMAX], g_uc[WF_GMAX], g_cs1[WF_GMAX];
-    int g_left[WF_GMAX];  // -1 idle, -2 waiting for the tile's previous chunk, -3/-4 claimed, >= 0 slots running
-    int band_k;
-    int exhausted;  // every band's units handed out
-    int abort;      // a ring entry never arrived (never expected): every wave leaves, the launch fails
-};
-// float4s per slot record: path state (8), running means (3), the volume (2, FT_VOL)
-__host__ __device__ constexpr int wf_rec_q(int F) { return (F & FT_VOL) ? 13 : 11; }
-struct WfAcc {  // a slot's pixel running means (trace_body's acc slots), in registers while it shades
-    float4 im;
-    v3 al, nr;
-    int hits;
-    float w;
-};
-template <int F>
-__device__ __forceinline__ void wf_store(float4* r, const Path& st, int pixel, int sample, const WfAcc& a) {
-    const unsigned long long s = st.rng.state, c = st.rng.inc;
-    r[0] = make_float4(st.o.x, st.o.y, st.o.z, st.d.x);
-    r[1] = make_float4(st.d.y, st.d.z, st.radiance.x, st.radiance.y);
-    r[2] = make_float4(st.radiance.z, st.weight.x, st.weight.y, st.weight.z);
-    r[3] = make_float4(__uint_as_float((unsigned)s), __uint_as_float((unsigned)(s >> 32)), __uint_as_float((unsigned)c),
-                       __uint_as_float((unsigned)(c >> 32)));
-    r[4] = make_float4(__int_as_float(st.bounce), __int_as_float(st.opbounce), __int_as_float(st.flags | st.phase << 8),
-                       st.max_roughness);
-    r[5] = make_float4(__int_as_float(st.li), __int_as_float(st.lcount), st.pb, st.pdf);
-    r[6] = make_float4(st.lpdf, st.lq.x, st.lq.y, st.lq.z);
-    r[7] = make_float4(__int_as_float(pixel), __int_as_float(sample), a.w, __int_as_float(a.hits));
-    r[8] = a.im;
-    r[9] = make_float4(a.al.x, a.al.y, a.al.z, a.nr.x);
-    r[10] = make_float4(a.nr.y, a.nr.z, 0.0f, 0.0f);
-    if (F & FT_VOL) {
-        r[11] = make_float4(st.vol.density.x, st.vol.density.y, st.vol.density.z, st.vol.scattering.x);
-        r[12] = make_float4(st.vol.scattering.y, st.vol.scattering.z, st.vol.scanisotropy, 0.0f);
-    }
-}
-template <int F>
-__device__ __forceinline__ void wf_load(const float4* r, Path& st, int& pixel, int& sample, WfAcc& a) {
-    const float4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6], q7 = r[7];
-    const float4 q8 = r[8], q9 = r[9], q10 = r[10];
-    st.o = V3(q0.x, q0.y, q0.z);
-    st.d = V3(q0.w, q1.x, q1.y);
-    st.radiance = V3(q1.z, q1.w, q2.x);
-    st.weight = V3(q2.y, q2.z, q2.w);
-    st.rng.state = (unsigned long long)__float_as_uint(q3.x) | (unsigned long long)__float_as_uint(q3.y) << 32;
-    st.rng.inc = (unsigned long long)__float_as_uint(q3.z) | (unsigned long long)__float_as_uint(q3.w) << 32;
-    st.bounce = __float_as_int(q4.x);
-    st.opbounce = __float_as_int(q4.y);
-    st.flags = __float_as_int(q4.z) & 0xff;
-    st.phase = __float_as_int(q4.z) >> 8;
-    st.max_roughness = q4.w;
-    st.li = __float_as_int(q5.x);
-    st.lcount = __float_as_int(q5.y);
-    st.pb = q5.z;
-    st.pdf = q5.w;
-    st.lpdf = q6.x;
-    st.lq = V3(q6.y, q6.z, q6.w);
-    pixel = __float_as_int(q7.x);
-    sample = __float_as_int(q7.y);
-    a.w = q7.z;
-    a.hits = __float_as_int(q7.w);
-    a.im = q8;
-    a.al = V3(q9.x, q9.y, q9.z);
-    a.nr = V3(q9.w, q10.x, q10.y);
-    if (F & FT_VOL) {
-        const float4 v0 = r[11], v1 = r[12];
-        st.vol.density = V3(v0.x, v0.y, v0.z);
-        st.vol.scattering = V3(v0.w, v1.x, v1.y);
-        st.vol.scanisotropy = v1.z;
-    }
-}
-
-// the WF body's AOV accessor: the slot's running means in registers (same float operations as
-// aov_update's LDS form)
-struct WfAov {
-    WfAcc* acc;
-    template <int F>
-    __device__ __forceinline__ float w() const { return acc->w; }
-};
-template <int F>
-__device__ __forceinline__ void aov_update(const WfAov& a, v3 ta, v3 tn) {
-    WfAcc& c = *a.acc;
-    const float aw = c.w;
-    const float omw = 1 - aw;
-    c.al = V3(c.al.x * omw + ta.x * aw, c.al.y * omw + ta.y * aw, c.al.z * omw + ta.z * aw);
-    c.nr = V3(c.nr.x * omw + tn.x * aw, c.nr.y * omw + tn.y * aw, c.nr.z * omw + tn.z * aw);
-}
-
-__device__ __forceinline__ int lane_rank(unsigned long long m) {  // active lanes of m below this lane
-    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
-__device__ __forceinline__ unsigned lds_ld(const unsigned* a) {
-    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ int lds_ld(const int* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-// LDS writes issued before this point reach LDS before any later LDS access of this wave, and
-// the compiler keeps them in order (a wave's LDS operations execute in issue order)
-__device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-// claim up to `want` entries of ring q (wave-uniform count); read them with wf_take
-__device__ __forceinline__ int wf_claim(WfCtl& C, int q, int want, unsigned& base) {
-    unsigned h = 0;
-    int n = 0;
-    if ((threadIdx.x & 63) == 0) {
-        for (;;) {
-            h = lds_ld(&C.head[q]);
-            const unsigned t = lds_ld(&C.tail[q]);
-            n = (int)(t - h) < want ? (int)(t - h) : want;
-            if (n <= 0) {
-                n = 0;
-                break;
-            }
-            unsigned expect = h;
-            if (__hip_atomic_compare_exchange_strong(&C.head[q], &expect, h + (unsigned)n, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-                break;
-        }
-    }
-    base = __builtin_amdgcn_readfirstlane(h);
-    return __builtin_amdgcn_readfirstlane(n);
-}
-// entry `idx` of a ring: its producer reserved it before writing it, so wait for the write
-// (bounded: a missing entry aborts the launch instead of hanging the GPU)
-__device__ __forceinline__ int wf_take(WfCtl& C, int* ring, unsigned idx) {
-    int s;
-    unsigned n = 0;
-    while ((s = __hip_atomic_load(ring + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < 0) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++n > (1u << 22)) {
-            __hip_atomic_store(&C.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return 0;
-        }
-    }
-    __hip_atomic_store(ring + idx, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return s;
-}
-// push this lane's slot onto ring q when `pred`; the caller has ordered what the consumer reads
-// (lds_order for LDS data, a workgroup release fence for the HBM record) before this
-__device__ __forceinline__ void wf_push(WfCtl& C, int* ring, int NP, int q, bool pred, int slot) {
-    const unsigned long long m = __builtin_amdgcn_ballot_w64(pred);
-    if (!m) return;
-    unsigned base = 0;
-    if ((threadIdx.x & 63) == 0) base = __hip_atomic_fetch_add(&C.tail[q], (unsigned)lane_count(m), __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (pred) __hip_atomic_store(ring + (base + (unsigned)lane_rank(m)) % (unsigned)NP, slot, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-#ifndef JT_WF_TRAV_ITERS
-#define JT_WF_TRAV_ITERS 8
-#endif
-
-template <int SAMPLER, int COUNT, int F, bool NCACHE>
-__device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A, int* stack,
-                              int* lds_wf, float4* pool) {
-    constexpr int RQ = wf_rec_q(F);
-    const int lane = threadIdx.x & 63;
-    const int G = P.wf_groups, NP = 64 * G;
-    __shared__ WfCtl C;
-    int* const ring[3] = {lds_wf, lds_wf + NP, lds_wf + 2 * NP};
-    float4* const q_o = reinterpret_cast<float4*>(lds_wf + 3 * NP);  // o.xyz, root bits
-    float4* const q_d = q_o + NP;                                       // d.xyz
-    float4* const r_h = q_d + NP;                                       // inst, elem, u, v
-    float* const r_t = reinterpret_cast<float*>(r_h + NP);              // t
-    float4* const recs = pool + (size_t)blockIdx.x * NP * RQ;
-    if (threadIdx.x < 3) {
-        C.head[threadIdx.x] = 0;
-        C.tail[threadIdx.x] = 0;
-    }
-    if (threadIdx.x < WF_GMAX) C.g_left[threadIdx.x] = -1;
-    if (threadIdx.x == 0) {
-        C.attn = (1u << G) - 1;
-        C.live = 0;
-        C.band_k = 0;
-        C.exhausted = 0;
-        C.abort = 0;
-    }
-    for (int k = threadIdx.x; k < 3 * NP; k += BLOCK) lds_wf[k] = -1;
-    __syncthreads();
-
-    Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    const int tiles_x = (P.width + 7) / 8, tiles = tiles_x * ((P.height + 7) / 8);
-    const int nchunks = num_chunks(P, s_begin, s_end);
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    Trav T;
-    T.sp = 0;
-    T.nprim = 0;
-    int qslot = -1;  // the slot whose query this lane runs (-1: none)
-    int pend = -1;   // a slot this lane shaded whose next query waits to be pushed (after its record store)
-    unsigned idle_iters = 0;
-#if JT_STAMPS
-    // diagnostic build: cycles per job kind, traversal lane counts, batch sizes (scripts/stamps.py wf)
-    unsigned long long sw[15] = {0};
-    unsigned long long tj = __builtin_amdgcn_s_memtime();
-#define WF_STAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sw[k] += t_ - tj; tj = t_; } while (0)
-#define WF_ADD(k, v) (sw[k] += (v))
-#else
-#define WF_STAMP(k) ((void)0)
-#define WF_ADD(k, v) ((void)0)
-#endif
-
-    // a slot's pending query (LDS): origin, direction, root
-    auto issue = [&](int s, const Path& st) {
-        const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
-        const v3 o = st.o;
-        const unsigned root = light ? (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance
-                                    : (T_TLAS << 30) | SNAP_NONE;
-        q_o[s] = make_float4(o.x, o.y, o.z, __uint_as_float(root));
-        q_d[s] = make_float4(st.d.x, st.d.y, st.d.z, 0.0f);
-        if (light) cnt.light_queries++;
-        else cnt.rays++;
-    };
-
-    // Roles: the last P.wf_shaders waves of the workgroup only shade and start slot groups; the
-    // others traverse, refilling their lanes from the ring, and shade too whenever they hold no
-    // query and none waits (work-conserving). A wave shades only with no query in flight, so it
-    // runs each path's sample_lights_pdf instance queries (short: one light's BLAS) inline on its
-    // own lanes' stacks right after path_hit, with the path in registers: only closest-hit scene
-    // queries go through the rings.
-    const bool shader = (int)(threadIdx.x >> 6) >= BLOCK / 64 - P.wf_shaders;
-    auto ctl = [&]() {  // one LDS round trip: the control words, one per lane, read by all
-        const unsigned cv = lane < 8 ? lds_ld(reinterpret_cast<const unsigned*>(&C) + lane) : 0u;
-        return cv;
-    };
-    auto finished_all = [&]() { return lds_ld(&C.exhausted) && lds_ld(&C.live) == 0u; };
-
-    for (;;) {
-        // queries issued by the last shading job: their records are stored, now publish them
-        if (__builtin_amdgcn_ballot_w64(pend >= 0)) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            wf_push(C, ring[WF_TRAV], NP, WF_TRAV, pend >= 0, pend);
-            pend = -1;
-        }
-        if (lds_ld(&C.abort)) break;
-        unsigned cv = ctl();
-        unsigned tq = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
-        const unsigned tl = tq;
-        const unsigned sl = __builtin_amdgcn_readlane(cv, 4) - __builtin_amdgcn_readlane(cv, 1);
-        const unsigned attn = __builtin_amdgcn_readlane(cv, 6);
-        int busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
-        if (!shader && (busy > 0 || tq > 0)) {
-            // ------------------------------------------------------------ traverse
-            idle_iters = 0;
-            WF_ADD(12, tq);
-            for (int it = 0; it < JT_WF_TRAV_ITERS; it++) {
-                // refill: lanes without a query take the oldest waiting ones (their first pop at once)
-                if (tq > 0 && (64 - busy >= P.wf_refill || busy == 0)) {
-                    unsigned base;
-                    const int n = wf_claim(C, WF_TRAV, 64 - busy, base);
-                    WF_ADD(9, 1);
-                    WF_ADD(10, n);
-                    if (n > 0) {
-                        const int r = lane_rank(__builtin_amdgcn_ballot_w64(qslot < 0));
-                        if (qslot < 0 && r < n) {
-                            const int s = wf_take(C, ring[WF_TRAV], (base + (unsigned)r) % (unsigned)NP);
-                            const float4 o = q_o[s], d = q_d[s];
-                            qslot = s;
-                            query_begin(T, V3(o.x, o.y, o.z), V3(d.x, d.y, d.z), __float_as_uint(o.w), stack);
-#pragma unroll
-                            for (int k = 0; k < JT_FIRST_POP; k++)
-                                if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
-                        }
-                    }
-                }
-                const bool wantp = T.nprim > 0;
-                const bool wantn = T.nprim == 0 && T.sp > 0;
-                const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
-                const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
-                WF_ADD(4, 1);
-                WF_ADD(5, np >= nn ? np : nn);
-                WF_ADD(6, np + nn);
-                if (np >= nn) {
-                    if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < JT_NODE_REPEAT; k++)
-                        if (T.nprim == 0 && T.sp > 0) node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
-                }
-                // finished queries: the result to LDS, the slot onto the shading ring
-                const bool fin = qslot >= 0 && (T.sp | T.nprim) == 0;
-                if (__builtin_amdgcn_ballot_w64(fin)) {
-                    if (fin) {
-                        r_h[qslot] = make_float4(__int_as_float(T.h_inst), __int_as_float(T.h_elem), T.h_u, T.h_v);
-                        r_t[qslot] = T.tmax;
-                    }
-                    lds_order();
-                    wf_push(C, ring[WF_SCENE], NP, WF_SCENE, fin, qslot);
-                    if (fin) qslot = -1;
-                }
-                busy = lane_count(__builtin_amdgcn_ballot_w64(qslot >= 0));
-                cv = ctl();
-                tq = __builtin_amdgcn_readlane(cv, 3) - __builtin_amdgcn_readlane(cv, 0);
-                if (busy == 0 && tq == 0) break;
-            }
-            WF_STAMP(0);
-            continue;
-        }
-        // this wave holds no query: start a group, shade, or wait
-        int gsel = -1;
-        if (attn) {  // a group to start: an idle one while units remain, or one whose tile is ready
-            if (lane == 0) {
-                for (int g = 0; g < G && gsel < 0; g++) {
-                    if (!((attn >> g) & 1)) continue;
-                    const int gl = lds_ld(&C.g_left[g]);
-                    int expect = gl;
-                    if (gl == -2) {
-                        if (__hip_atomic_load(A.tile_done + C.g_tile[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= C.g_uc[g] &&
-                            __hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
-                            gsel = g;
-                    } else if (gl == -1) {
-                        if (__hip_atomic_compare_exchange_strong(&C.g_left[g], &expect, -4, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                            gsel = g;
-                            __hip_atomic_fetch_add(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                    }
-                    if (gsel >= 0) __hip_atomic_fetch_and(&C.attn, ~(1u << g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-            gsel = __builtin_amdgcn_readfirstlane(gsel);
-        }
-        WF_STAMP(14);
-        WF_ADD(13, 1);
-        if (gsel >= 0) {
-            // ------------------------------------------------------------ start a slot group
-            const int g = gsel;
-            int state = 0;
-            if (lane == 0) {
-                state = C.g_left[g];
-                if (state == -4) {  // idle group: fetch a unit (this XCD's band first, then the others)
-                    int unit_uc = -1, unit_t = 0;
-                    for (;;) {
-                        const int bk = lds_ld(&C.band_k);
-                        if (bk >= NBANDS) break;
-                        const int band = (int)((xcc + (unsigned)bk) & (NBANDS - 1));
-                        const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
-                        const unsigned unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
-                        if (unit < (unsigned)bn * (unsigned)nchunks) {
-                            unit_uc = (int)(unit / (unsigned)bn);
-                            unit_t = bt0 + (int)(unit % (unsigned)bn);
-                            break;
-                        }
-                        int expect = bk;
-                        __hip_atomic_compare_exchange_strong(&C.band_k, &expect, bk + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                    if (unit_uc < 0) {  // no units left: this group stays idle
-                        __hip_atomic_store(&C.exhausted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_sub(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        state = -1;
-                    } else {
-                        C.g_tile[g] = unit_t;
-                        C.g_uc[g] = unit_uc;
-                        int cs0, cs1;
-                        chunk_range(P, s_begin, s_end, unit_uc, cs0, cs1);
-                        C.g_cs1[g] = cs1;
-                        if (unit_uc > 0 &&
-                            __hip_atomic_load(A.tile_done + unit_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unit_uc) {
-                            // its tile's previous chunk is not published yet: start it later
-                            __hip_atomic_store(&C.g_left[g], -2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            state = -2;
-                        }
-                    }
-                }
-            }
-            state = __builtin_amdgcn_readfirstlane(state);
-            if (state == -1 || state == -2) continue;
-            lds_order();
-            const int ut = C.g_tile[g], uc = C.g_uc[g];
-            if (uc > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous chunk's running means
-            const int i = (ut % tiles_x) * 8 + (lane & 7), j = (ut / tiles_x) * 8 + (lane >> 3);
-            const bool in_image = i < P.width && j < P.height;
-            const int s = g * 64 + lane;
-            int cs0, cs1u;
-            chunk_range(P, s_begin, s_end, uc, cs0, cs1u);
-            (void)cs1u;
-            const int pixel = j * P.width + i;
-            if (in_image) {
-                const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
-                WfAcc acc{im, V3(al.x, al.y, al.z), V3(nr.x, nr.y, nr.z), 0, 1.0f / (float)(cs0 - P.first + 1)};
-                Path st;
-                start_path(P, i, j, pixel, cs0, st);
-                wf_store<F>(recs + (size_t)s * RQ, st, pixel, cs0, acc);
-                issue(s, st);
-                pend = s;
-            }
-            const int started = lane_count(__builtin_amdgcn_ballot_w64(in_image));
-            if (lane == 0) __hip_atomic_store(&C.g_left[g], started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            WF_STAMP(2);
-            continue;
-        }
-        // a shading wave shades when a full batch waits or the traversal waves are about to run
-        // dry; a traversal wave without queries shades whatever waits
-        if (!(sl >= (unsigned)P.wait_lanes || (sl > 0 && (!shader || tl < (unsigned)P.wf_refill * 4)))) {
-            if (sl == 0 && tl == 0 && finished_all()) break;
-            __builtin_amdgcn_s_sleep(1);
-            if (++idle_iters > (1u << 27)) {  // bounded: never expected
-                if (lane == 0) atomicAdd(A.counters + 7, 1ull);
-                break;
-            }
-            WF_STAMP(3);
-            continue;
-        }
-        idle_iters = 0;
-        // ------------------------------------------------------------ shade a batch
-        unsigned base;
-        const int n = wf_claim(C, WF_SCENE, 64, base);
-        if (n == 0) continue;
-        WF_ADD(7, 1);
-        WF_ADD(8, n);
-        const bool mine = lane < n;
-        int s = -1;
-        bool alive = false;
-        if (mine) {
-            s = wf_take(C, ring[WF_SCENE], (base + (unsigned)lane) % (unsigned)NP);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            Path st;
-            WfAcc acc;
-            int pixel, sample;
-            wf_load<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
-            const float4 hh = r_h[s];
-            const Hit h{__float_as_int(hh.x), __float_as_int(hh.y), hh.z, hh.w, r_t[s], __float_as_int(hh.x) >= 0};
-            const WfAov aov{&acc};
-            bool done;
-            if (SAMPLER == 2) done = naive_hit<F>(S, P, st, h, aov, cnt.shades);
-            else done = path_hit<F>(S, P, st, h, aov, cnt.shades);
-            // sample_lights_pdf's instance queries, inline (src/trace.jl:1018-1044)
-            while (SAMPLER == 1 && !done && st.phase == PH_LIGHT) {
-                cnt.light_queries++;
-                query_begin(T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
-                while (T.sp > 0 || T.nprim > 0) {
-                    if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-                    else node_step<16, false, COUNT, NCACHE, F>(S, T, stack, 0, cnt);
-                }
-                done = light_hit<F>(S, P, st, query_hit(T));
-            }
-            alive = true;
-            if (done) {
-                // trace_sample's epilogue (src/trace.jl:625-648) on the slot's running means
-                cnt.paths++;
-                v3 radiance = st.radiance;
-                if (!all_finite(radiance)) radiance = V3(0, 0, 0);
-                const float mr = max3(radiance);
-                if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
-                const float w = acc.w;
-                const float omw = 1 - w;
-                const bool hit = st.flags & F_HIT;
-                const bool env = !hit && !P.envhidden && S.nenvs != 0;
-                const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
-                if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
-                acc.im.x = acc.im.x * omw + target.x * w;
-                acc.im.y = acc.im.y * omw + target.y * w;
-                acc.im.z = acc.im.z * omw + target.z * w;
-                acc.im.w = acc.im.w * omw + target.w * w;
-                if (hit || env) acc.hits += 1;
-                if (++sample < C.g_cs1[s >> 6]) {
-                    acc.w = 1.0f / (float)(sample - P.first + 1);
-                    start_path(P, pixel % P.width, pixel / P.width, pixel, sample, st);
-                } else {  // the slot's chunk is done: its pixel's running means back to HBM
-                    alive = false;
-                    A.image[pixel] = acc.im;
-                    A.albedo[pixel] = make_float4(acc.al.x, acc.al.y, acc.al.z, 0.0f);
-                    A.normal[pixel] = make_float4(acc.nr.x, acc.nr.y, acc.nr.z, 0.0f);
-                    A.hits[pixel] += acc.hits;
-                }
-            }
-            if (alive) {
-                wf_store<F>(recs + (size_t)s * RQ, st, pixel, sample, acc);
-                issue(s, st);
-                pend = s;
-            }
-        }
-        // slots whose chunk is done: the last one of its group publishes the tile
-        const bool fin = mine && !alive;
-        if (__builtin_amdgcn_ballot_w64(fin)) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            bool last = false;
-            const int g = s >> 6;
-            if (fin) last = __hip_atomic_fetch_add(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 1;
-            if (__builtin_amdgcn_ballot_w64(last)) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                if (last) {
-                    if (C.g_uc[g] + 1 < nchunks)
-                        __hip_atomic_store(A.tile_done + C.g_tile[g], C.g_uc[g] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&C.g_left[g], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (!lds_ld(&C.exhausted))
-                        __hip_atomic_fetch_or(&C.attn, 1u << g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_sub(&C.live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-        }
-        WF_STAMP(1);
-    }
-#if JT_STAMPS
-    if (lane == 0)
-        for (int k = 0; k < 15; k++) atomicAdd(A.counters + 8 + k, sw[k]);
-#endif
-#undef WF_STAMP
-#undef WF_ADD
-    unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
-                     COUNT ? cnt.shades : 0u};
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-        unsigned sum = wave_sum(v[k]);
-        if (lane == 0 && sum) atomicAdd(&A.counters[k], (unsigned long long)sum);
-    }
-}
-
 // Occupancy request (waves per SIMD); JT_WAVES=0 leaves it to the compiler. The LDS-mode
 // FT_NONE kernel (cornellbox: 96 VGPRs, LDS for 5 workgroups per CU with the stack sized to the
 // scene) asks for JT_WAVES_NONE: measured +4 % over 4 waves with its wait_lanes of 56.
@@ -1878,16 +1300,6 @@ __device__ void trace_body_wf(const DScene& S, const DParams& P, int s_begin, in
 #define JT_WAVES_PER_EU
 #define JT_WAVES_PER_EU_F(F)
 #endif
-// WF kernels (trace_body_wf): occupancy request, 0 = the compiler's choice
-#ifndef JT_WAVES_WF
-#define JT_WAVES_WF 4
-#endif
-#if JT_WAVES_WF > 0
-#define JT_WAVES_PER_EU_WF __attribute__((amdgpu_waves_per_eu(JT_WAVES_WF, JT_WAVES_WF)))
-#else
-#define JT_WAVES_PER_EU_WF
-#endif
-
 // the scene arrays of the LDS blob (small-scene mode; offsets from jt_create)
 __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob) {
     DScene L = S;
@@ -1911,23 +1323,11 @@ __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob)
     return L;
 }
 
-// HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS. The
-// workgroup first copies the top nlnodes nodes (the breadth-first top of the TLAS, visited by
-// nearly every ray) into dynamic LDS: those node reads then skip the vector-memory path (TA/TD,
-// the measured limiter of this mode).
+// HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS.
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     __shared__ int lds_stack[RING * BLOCK];
-    __shared__ uint4 pop_lds[JT_POP_LDS ? BLOCK : 1];
-    extern __shared__ uint4 node_cache[];
-    const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
-    for (int k = threadIdx.x; k < 2 * S.nlnodes; k += BLOCK) node_cache[k] = src[k];
-    if (JT_POP_LDS) pop_lds[threadIdx.x] = make_uint4(~0u, 0u, 0u, 0u);
-    __syncthreads();
-    DScene L = S;
-    L.lnodes = reinterpret_cast<const DNode*>(node_cache);
-    L.pcl = pop_lds;
-    trace_body<SAMPLER, RING, OVF, COUNT, F, true>(L, P, s_begin, s_end, A, lds_stack + threadIdx.x);
+    trace_body<SAMPLER, RING, OVF, COUNT, F, true>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
 }
 
 // LDS mode (small scenes): the workgroup stages the scene blob into LDS once; every node,
@@ -1941,31 +1341,6 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(D
     __syncthreads();
     const DScene L = blob_scene(S, blob);
     trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
-}
-
-// WF kernels (trace_body_wf, stack bound <= 16): dynamic LDS = the lanes' stacks, the WF rings /
-// queries / results, then the scene blob (LDS mode) or nothing (HBM mode: the scene from L2).
-template <int SAMPLER, int COUNT, int F, bool LDSM>
-__global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_WF void trace_kernel_wf(DScene S, DParams P, int s_begin, int s_end,
-                                                                            DAccum A, float4* pool) {
-    extern __shared__ uint4 dyn_lds[];
-    const int NP = 64 * P.wf_groups;
-    int* const stack = reinterpret_cast<int*>(dyn_lds);
-    int* const wf = stack + S.stack_need * BLOCK;
-    uint4* const blob = reinterpret_cast<uint4*>(wf + 3 * NP) + 3 * NP + NP / 4;
-    DScene L = S;
-    if (LDSM) {
-        for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
-        __syncthreads();
-        L = blob_scene(S, blob);
-    }
-    L.nlnodes = 0;
-    __shared__ uint4 pop_lds[JT_POP_LDS ? BLOCK : 1];
-    if (JT_POP_LDS) {
-        pop_lds[threadIdx.x] = make_uint4(~0u, 0u, 0u, 0u);
-        L.pcl = pop_lds;
-    }
-    trace_body_wf<SAMPLER, COUNT, F, !LDSM>(L, P, s_begin, s_end, A, stack + threadIdx.x, wf, pool);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of
@@ -1989,34 +1364,9 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
         }
     }
     const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT, F>;
-    const size_t cache = (size_t)S.nlnodes * sizeof(DNode);
-    if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cache)) != hipSuccess) return e;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, cache) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     const int nwg = std::min(want, per_cu * cus);
-    hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), cache, st, S, P, s0, s1, A);
-    return hipGetLastError();
-}
-
-// WF launch (trace_body_wf): every resident workgroup, each with wf_groups * 64 path slots
-template <int SAMPLER, int COUNT, int F>
-hipError_t launch_wf(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
-    const int NP = 64 * P.wf_groups;
-    const bool ldsm = S.blob_n16 > 0;
-    const size_t lds = (size_t)S.stack_need * BLOCK * 4 + (size_t)NP * (3 * 4 + 3 * 16 + 4) +
-                       (ldsm ? (size_t)S.blob_n16 * 16 : 0);
-    const void* k = ldsm ? (const void*)trace_kernel_wf<SAMPLER, COUNT, F, true>
-                         : (const void*)trace_kernel_wf<SAMPLER, COUNT, F, false>;
-    hipError_t e;
-    if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-    const size_t rec = (size_t)NP * wf_rec_q(F) * 16;
-    const int nwg = (int)std::min<size_t>((size_t)per_cu * cus, A.pool_bytes / rec);
-    if (nwg < 1) return hipErrorInvalidValue;
-    if (ldsm)
-        hipLaunchKernelGGL((trace_kernel_wf<SAMPLER, COUNT, F, true>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A, A.pool);
-    else
-        hipLaunchKernelGGL((trace_kernel_wf<SAMPLER, COUNT, F, false>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A, A.pool);
+    hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
     return hipGetLastError();
 }
 
@@ -2052,10 +1402,6 @@ hipError_t launch_s(int need, int ring, int kmask, const DScene& S, const DParam
     return launch_t<1, 16, JT_ONE_OVF, 0, JT_ONE_FEAT, !JT_ONE_OVF>(S, P, s0, s1, A, st, cus);
 #else
     if (need <= 16) {
-        if (P.wf_groups > 0) {
-            if (kmask == FT_NONE) return launch_wf<SAMPLER, COUNT, FT_NONE>(S, P, s0, s1, A, st, cus);
-            return launch_wf<SAMPLER, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
-        }
         if (kmask == FT_NONE) return launch_t<SAMPLER, 16, false, COUNT, FT_NONE>(S, P, s0, s1, A, st, cus);
         return launch_t<SAMPLER, 16, false, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
     }
@@ -2430,8 +1776,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
 
     // ------------------------------------------------------------- flatten to the HBM layout
     // The TLAS is stored breadth-first (sibling pairs stay adjacent, the root stays node 0), so its
-    // top levels are one prefix of the node array — the prefix HBM mode caches in LDS. Storage
-    // order only: the traversal still visits the reference's nodes in the reference's order.
+    // top levels share cache lines. Storage order only: the traversal still visits the
+    // reference's nodes in the reference's order.
     std::vector<DNode> tlas;
     {
         const int tn = std::max(0, bvh->tlas.nnodes);
@@ -2747,8 +2093,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         // HBM mode's stack is the kernel's static ring (16 or 32 entries); LDS mode's, without
         // overflow, just the scene's bound
         const size_t acc_bytes = (size_t)ACC_SLOTS * BLOCK * 4;
-        const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 4 + acc_bytes +
-                                  (JT_POP_LDS ? (size_t)BLOCK * 16 : 0);
+        const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 4 + acc_bytes;
         const size_t lds_base = (size_t)(c->stack <= 16 ? c->stack : c->ring) * BLOCK * 4 + acc_bytes;
         const size_t bytes = blob.size() * 16;
         const size_t lds_cu = 160 * 1024;
@@ -2761,16 +2106,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             S.blob_n16 = (int)blob.size();
         }
         c->lds_scene_bytes = S.blob_n16 ? bytes : 0;
-        // HBM mode: cache the breadth-first top of the TLAS in what LDS is left at 4 workgroups
-        // per CU (160 KiB / 4 minus the stack ring and the running means); JT_NODE_CACHE caps it
-        S.lnodes = nullptr;
-        S.nlnodes = 0;
-        if (!S.blob_n16 && JT_TLAS_LDS) {
-            const long left = (long)(lds_cu / 4) - (long)base_bytes;
-            long n = std::min<long>((long)tlas.size(), std::max<long>(0, left) / (long)sizeof(DNode));
-            if (const char* v = std::getenv("JT_NODE_CACHE")) n = std::min<long>(n, std::max(0, std::atoi(v)));
-            S.nlnodes = (int)n;
-        }
     }
     S.ovf = nullptr;
     S.ovf_stride = 0;
@@ -2834,20 +2169,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
     P.light_lanes = 2;
     if (const char* ll = std::getenv("JT_LIGHT_LANES")) P.light_lanes = std::max(1, std::min(65, std::atoi(ll)));
-    // WF body (trace_body_wf): scenes whose stack bound fits the lanes' 16-entry LDS stacks
-    P.wf_groups = 0;
-    if (const char* wf = std::getenv("JT_WF")) {
-        if (std::atoi(wf) > 0 && c->stack <= 16) {
-            P.wf_groups = 5;
-            if (const char* g = std::getenv("JT_WF_GROUPS")) P.wf_groups = std::max(1, std::min(WF_GMAX, std::atoi(g)));
-            P.wait_lanes = 56;
-            if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
-            P.wf_refill = 8;
-            if (const char* r = std::getenv("JT_WF_REFILL")) P.wf_refill = std::max(1, std::min(64, std::atoi(r)));
-            P.wf_shaders = 1;
-            if (const char* r = std::getenv("JT_WF_SHADERS")) P.wf_shaders = std::max(1, std::min(3, std::atoi(r)));
-        }
-    }
 
     // accumulators (make_trace_state: zeroed) + counters
     const size_t np = (size_t)W * (size_t)H;
@@ -2871,23 +2192,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, params->device) == hipSuccess && cus > 0) c->cus = cus;
     c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt,
-                  (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE, nullptr, 0};
-    if (JT_ACC_HBM && P.wf_groups == 0) {  // running-mean slots: at most 8 workgroups of 256 lanes per CU
-        const size_t bytes = (size_t)c->cus * 8 * 11 * BLOCK * 4;
-        void* pool = nullptr;
-        if ((e = hipMalloc(&pool, bytes)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc running-mean slots"));
-        c->allocations.push_back(pool);
-        c->A.pool = (float4*)pool;
-        c->A.pool_bytes = bytes;
-    }
-    if (P.wf_groups > 0) {  // path-slot records: at most 8 workgroups of 256 lanes per CU
-        const size_t bytes = (size_t)c->cus * 8 * 64 * WF_GMAX * wf_rec_q(FT_ALL) * 16;
-        void* pool = nullptr;
-        if ((e = hipMalloc(&pool, bytes)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc WF path records"));
-        c->allocations.push_back(pool);
-        c->A.pool = (float4*)pool;
-        c->A.pool_bytes = bytes;
-    }
+                  (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE};
     st = jt_reset(c);
     if (st != JT_OK) return bail(st);
     *out = c;
@@ -3289,10 +2594,10 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     char tmp[512];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d wf_groups=%d env_alias=%d",
-                  c->P.wf_groups ? "trace_kernel_wf" : c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
+                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d env_alias=%d",
+                  c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, c->kmask, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
-                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->P.nct, c->tiles, BLOCK, c->P.wf_groups,
+                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->P.nct, c->tiles, BLOCK,
                   c->env_alias ? 1 : 0);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;

@@ -169,32 +169,6 @@ def test_feature_specialisation_bitwise_equal(gpu, abi, lib, cornell_abi, sample
         assert outs[0][2][k] == outs[1][2][k], k
 
 
-@pytest.mark.parametrize("sampler", [1, 2])
-def test_tlas_node_cache_is_bitwise_invariant(gpu, abi, lib, cornell_abi, sampler, monkeypatch):
-    """HBM mode can read the breadth-first top of the TLAS from an LDS copy (built with
-    JT_TLAS_LDS=1; the default build compiles the cache out): none, part or all of it
-    cached gives the same bits (the node order in memory is storage only)."""
-    from jtrace import trace
-    bvh = trace.make_scene_bvh(cornell_abi, False, lib)
-    lights = trace.make_trace_lights(cornell_abi, lib)
-    p = make_params(abi, resolution=64, samples=4, sampler=sampler)
-    monkeypatch.setenv("JT_LDS_SCENE", "0")
-    outs = []
-    for n in ("0", "2", "100000"):
-        monkeypatch.setenv("JT_NODE_CACHE", n)
-        st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
-        st.set_counters(1)
-        st.trace_range(0, 4)
-        outs.append((st.get_image(), st.get_aovs(), st.counters()))
-        st.close()
-    for o in outs[1:]:
-        assert np.array_equal(outs[0][0], o[0])
-        for a, b in zip(outs[0][1], o[1]):
-            assert np.array_equal(a, b)
-        for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades"):
-            assert outs[0][2][k] == o[2][k], k
-
-
 def test_light_hit_steps_are_bitwise_invariant(gpu, abi, lib, cornell_abi, monkeypatch):
     """Light-hit steps inside the traversal phase (FT_NONE kernel, path sampler) only change
     when a lane runs light_hit, not what it computes: every threshold gives the same bits."""
