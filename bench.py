@@ -58,16 +58,19 @@ def shade_record_bytes(scene) -> int:
     return best
 
 
-def roofline_record(workload: str, kernel: str):
+def roofline_record(workload: str, kernel: str, build: str):
     """The committed roofline record (profiles/*_roofline/*.json, written on the GPU box by
     scripts/roofline.py from rocprofv3 kernel-trace + PMC passes of this same bench command) for
-    this workload and kernel instance, newest round first; (None, None) when none matches."""
+    this workload, kernel instance and build (scripts/roofline.py source_hash), newest round
+    first; (None, None) when none matches. A record of another build is never used: its counts
+    describe other code."""
     for f in sorted((ROOT / "profiles").glob("*_roofline/*.json"), reverse=True):
         try:
             d = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
-        if d.get("workload") == workload and d.get("kernel", "").replace(" ", "") == kernel.replace(" ", ""):
+        if d.get("workload") == workload and d.get("kernel", "").replace(" ", "") == kernel.replace(" ", "") \
+                and d.get("build") == build:
             return d, str(f.relative_to(ROOT))
     return None, None
 
@@ -100,6 +103,8 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--sampler", default="path")
     ap.add_argument("--scene", default=str(ROOT / "assets" / "scenes" / "cornellbox" / "cornellbox.json"))
+    ap.add_argument("--traversal", choices=["reference", "near"], default="reference",
+                    help="BVH child order (include/jtrace.h jt_traversal); the headline uses the reference's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-spp", type=int, default=128)
@@ -135,7 +140,7 @@ def main():
     sa = abi.SceneABI(scene)
     t_load = time.perf_counter()
     params = Params(scene=args.scene, samples=args.spp, sampler=2 if args.sampler == "naive" else 1,
-                    width=args.width, height=args.height, device=dev, batch=args.spp)
+                    width=args.width, height=args.height, device=dev, batch=args.spp, traversal=args.traversal)
     jp = abi.make_params(params, 0)
     bvh = trace.make_scene_bvh(sa, False, lib)
     t_bvh = time.perf_counter()
@@ -232,45 +237,66 @@ def main():
         per_launch = {k: v / max(1, full["launches"]) for k, v in full.items()}  # one step's launches
         logical = algorithmic_bytes(per_launch, shade_record_bytes(scene),
                                     any(len(s.quads) for s in scene.shapes))
-        workload = f"{name} {args.sampler} {W}x{H} {s1 - s0} samples/launch"
-        rec, rec_src = roofline_record(workload, kernel)
-        # HBM roof with MEASURED bytes: the PMC traffic per launch of this kernel on this workload
-        # (committed record) over this run's launch time. The §8(d) algorithmic bytes are reported
-        # beside it: small scenes serve them from LDS, so they are not HBM bytes.
-        traffic = rec["derived"]["traffic_bytes"] if rec else None
-        achieved = traffic / avg_launch_s / 1e9 if traffic else None
-        binding = None
+        workload = f"{name} {args.sampler} {W}x{H} {s1 - s0} samples/launch" + \
+            ("" if args.traversal == "reference" else f" traversal={args.traversal}")
+        sys.path.insert(0, str(ROOT / "scripts"))
+        from roofline import VMEM_PEAK_GIPS, source_hash
+        build = source_hash()
+        rec, rec_src = roofline_record(workload, kernel, build)
+        # The roof that binds, from the PMC counts of this kernel on this workload and build
+        # (committed record) over THIS run's launch time (HIP events):
+        #  - LDS mode (small scenes: the scene is in LDS): VALU issue of partly idle waves —
+        #    achieved = useful FP32 lane-operations per second, peak = the CUs' FP32 lane rate;
+        #  - HBM mode (node / primitive records L2-resident): the vector-memory return path (TD) —
+        #    achieved = vector-memory read wave-instructions per second, peak = the measured
+        #    dwordx4 gather ceiling (profiles/r02_pair/td_width_bench.log).
+        # HBM itself (measured traffic / 8 TB/s) is reported beside it as hbm_frac.
+        lds_mode = "mode=lds" in desc
+        roof = {"bound": "valu" if lds_mode else "vmem/TD", "achieved": None, "peak": None,
+                "unit": "G lane-ops/s" if lds_mode else "G wave-instr/s", "frac": None, "traffic": None,
+                "hbm_achieved_gbs": None, "hbm_peak_gbs": HBM_PEAK_GBS, "hbm_frac": None,
+                "source": rec_src, "build": build, "kernel": kernel, "launch": desc,
+                "avg_launch_ms": round(avg_launch_s * 1e3, 3), "binding": None}
         if rec:
             d = rec["derived"]
-            binding = {k: d[k] for k in ("valu_issue_frac", "lane_util", "fp32_lane_frac", "td_busy_frac",
-                                         "clock_ghz") if k in d}
-            # LDS mode (small scenes): the scene is in LDS, VALU issue of partly idle waves binds;
-            # HBM mode: node/primitive loads through the vector-memory return path (TD) bind
-            binding["resource"] = ("vector-memory return path (TD)" if "mode=hbm" in desc
-                                   else "VALU issue of divergent waves")
-            binding["write_bytes_per_launch"] = int(d["write_bytes"])
-            binding["profiled_launch_ms"] = round(rec["duration_ns"] / 1e6, 3)
-        roof = {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None if traffic is None else int(traffic), "source": rec_src,
-                "kernel": kernel, "launch": desc, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                "binding": binding,
+            if lds_mode and "valu_lane_ops" in d:
+                achieved, peak = d["valu_lane_ops"] / avg_launch_s / 1e9, d["valu_peak_gops"]
+            elif not lds_mode and "vmem_rd_per_launch" in d:
+                achieved, peak = d["vmem_rd_per_launch"] / avg_launch_s / 1e9, VMEM_PEAK_GIPS
+            else:
+                achieved = peak = None
+            if achieved is not None:
+                roof.update(achieved=round(achieved, 2), peak=round(peak, 2), frac=round(achieved / peak, 5))
+            traffic = d["traffic_bytes"]  # measured HBM bytes per launch (PMC, gfx950-corrected)
+            roof.update(traffic=int(traffic), hbm_achieved_gbs=round(traffic / avg_launch_s / 1e9, 1),
+                        hbm_frac=round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5))
+            roof["binding"] = {k: d[k] for k in ("valu_issue_frac", "lane_util", "fp32_lane_frac", "td_busy_frac",
+                                                 "vmem_frac", "clock_ghz") if k in d}
+            roof["binding"]["write_bytes_per_launch"] = int(d["write_bytes"])
+            roof["binding"]["profiled_launch_ms"] = round(rec["duration_ns"] / 1e6, 3)
+        alg_gbs = logical / avg_launch_s / 1e9
+        roof.update({
                 "algorithmic": {"bytes_per_launch": int(logical),
                                 "bytes_per_ray": round(logical / max(1.0, per_launch["rays"]), 1),
-                                "gbs": round(logical / avg_launch_s / 1e9, 1),
-                                "note": "SURVEY §8(d) logical bytes (node/instance/primitive/shading records); "
-                                        "served from LDS/L2, not HBM"},
+                                "gbs": round(alg_gbs, 1),
+                                "note": "SURVEY §8(d) logical bytes (node/instance/primitive/shading records) "
+                                        "over the launch time; served from LDS (small scenes) or L2, not HBM"
+                                        + (f": {alg_gbs / 1e3:.1f} TB/s exceeds the 8 TB/s HBM peak, so HBM is not "
+                                           "this kernel's roof" if alg_gbs > HBM_PEAK_GBS else "")},
                 # traversal work per closest-hit query, from the counting pass
                 "per_ray": {k: round(per_launch[k] / max(1.0, per_launch["rays"]), 3)
-                            for k in ("nodes", "instances", "prims", "shades", "light_queries")}}
+                            for k in ("nodes", "instances", "prims", "shades", "light_queries")}})
         line = {
-            "metric": metric_name(name, args.sampler, W, H, S), "value": round(value, 2), "unit": "Mrays/s",
+            "metric": metric_name(name, args.sampler, W, H, S) + ("" if args.traversal == "reference" else
+                                                                   f" (traversal={args.traversal})"),
+            "value": round(value, 2), "unit": "Mrays/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": f"scene: the reference's own {name} (assets/scenes/{name}), seed 0x5EED"
                     + (f"; {'; '.join(scene.notes)}" if scene.notes else ""),
             "config": {"workload": f"{name} {args.sampler} {W}x{H}x{S}spp", "scene": name,
                        "sampler": args.sampler, "width": W, "height": H, "spp": S, "bounces": 8,
+                       "traversal": args.traversal,
                        "parallelism": f"sample-range shards x{world} + RCCL reduce"},
             "render_s": round(ms_per_step / 1e3, 4),
             "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 2),

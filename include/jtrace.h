@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define JT_ABI_VERSION 1
+#define JT_ABI_VERSION 2
 
 typedef enum jt_status {
     JT_OK = 0,
@@ -69,6 +69,17 @@ typedef enum jt_material_type {
 
 /* Samplers, index into SAMPLER_TYPES = ["path", "naive"] (src/cli.jl:88). */
 typedef enum jt_sampler { JT_SAMPLER_PATH = 1, JT_SAMPLER_NAIVE = 2 } jt_sampler;
+
+/* BVH child visit order (extension, jt_params.traversal).
+ * JT_TRAVERSAL_REFERENCE: the reference's (src/bvh.jl:331-341, 396-407): for d[axis] >= 0 push
+ *   start then start+1, so the upper child (start+1, higher split-axis coordinates: split_middle /
+ *   split_sah partition lower centers to `start`, src/bvh.jl:171-176, 281-304) is visited first —
+ *   the far child for a closest-hit query.
+ * JT_TRAVERSAL_NEAR: the opposite push order, the near child by the split axis first. The closest
+ *   hit is the same up to ties: among hits at exactly equal t the later-tested wins
+ *   (src/geometry.jl:226, t > tmax rejects), so only exact-t ties (and a box culled by the slab
+ *   test's rounding) can resolve differently. Fewer nodes are visited (tmax shrinks sooner). */
+typedef enum jt_traversal { JT_TRAVERSAL_REFERENCE = 0, JT_TRAVERSAL_NEAR = 1 } jt_traversal;
 
 /* CameraData (src/scene.jl:48-86), after the lookat conversion done by the loader. */
 typedef struct jt_camera {
@@ -205,6 +216,7 @@ typedef struct jt_params {
     int32_t bvhstacksize;
     int32_t device;      /* HIP device ordinal for this context */
     uint64_t seed;       /* extension: RNG seed; stream keyed by (seed, pixel, global sample) */
+    int32_t traversal;   /* extension: jt_traversal (0 = the reference's child order) */
 } jt_params;
 
 /* Device counters accumulated over every launch of a context (diagnostic, exact). */

@@ -123,7 +123,8 @@ struct DScene {
     const float2* alias;    // DLight alias tables: (keep probability, alias index bits) per texel
     const float* srgb_lut;  // srgb_to_rgb(byte_to_float(b)), 256 entries (src/color.jl:12-23)
     const float* byte_lut;  // byte_to_float(b)
-    int tlas_nnodes, nenvs, nlights, pad;
+    int tlas_nnodes, nenvs, nlights;
+    int order_flip;  // jt_params.traversal: 0 the reference's child order, 7 the near child first
     // Small-scene mode: every array above that the traversal and shading read per step, packed
     // in one 16-B aligned blob the workgroup copies into LDS at kernel start (offsets in 16-B
     // units; -1 = not in the blob). Texels, environments and LUTs stay in HBM.
@@ -161,6 +162,9 @@ struct DParams {
     // full chunks, then a halving tail that shortens the launch's last units (JT_CHUNK_MIN)
     int nct;
     int cbeg[JT_MAX_CHUNKS + 1];
+    // the 8x8 tiles this launch covers: t = k * tile_stride + tile_offset (a multi-device context
+    // split by pixel tiles, jt_create_multi; 1 / 0 otherwise: every tile)
+    int tile_stride, tile_offset;
     unsigned long long seed;
 };
 

@@ -1,18 +1,6 @@
-// jt_trace.hip — the MI355X (gfx950) path-tracing megakernel and the C-ABI device context.
-//
-// Replaces trace_samples (Princic-1837592/julia-raytracer src/trace.jl:215-274) and everything
-// it calls per (pixel, sample, bounce): trace_sample :584, trace_path :276 / trace_naive :471,
-// intersect_scene_bvh / intersect_shape_bvh / intersect_instance_bvh (src/bvh.jl:306-520),
-// scene evaluation (src/scene.jl:372-928), shading (src/shading.jl), sampling (src/sampling.jl).
-//
-// Design: one lane owns one pixel and loops over its samples with path
-// regeneration — a lane whose path terminated starts its next sample in the same loop
-// iteration in which other lanes continue bouncing, so the wave stays full. Two-level BVH
-// traversal is one loop over a unified per-lane stack in LDS (TLAS nodes, instance entries,
-// BLAS nodes) so that every lane does one stack pop per iteration whatever level it is at;
-// the traversal order (and hence hit tie-breaking) is exactly the reference's. The running
-// mean (lerp with w = 1/(s+1), src/trace.jl:631-648) is kept in registers across samples and
-// written once per launch.
+// jt_trace.hip — the C-ABI device context of the MI355X path tracer (include/jtrace.h): scene
+// upload and layout, launches, the multi-device split and its RCCL reduce. The kernels are in
+// jt_kernels.h (instantiated by jt_kv.hip, one translation unit per configuration).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -25,1400 +13,41 @@
 #include <string>
 #include <vector>
 
-#include "jt_bsdf.h"
-#include "jt_device.h"
 #include "jt_internal.h"
-
-#ifndef JT_STAMPS
-#define JT_STAMPS 0
-#endif
-// pops per node iteration: the LDS-mode FT_NONE kernel (cornellbox) gains with 4 (+1.2 %),
-// the HBM-mode mesh kernels lose with 4 or 2 (bathroom1 -4 %, ecosys -1.5 %; gpurun_out/ab_nr)
-#ifndef JT_NODE_REPEAT_NONE
-#define JT_NODE_REPEAT_NONE 4
-#endif
-#ifndef JT_NODE_REPEAT
-#define JT_NODE_REPEAT 3
-#endif
-#ifndef JT_FIRST_POP
-#define JT_FIRST_POP 1
-#endif
-#ifndef JT_CHILD_PRETEST
-#define JT_CHILD_PRETEST 1
-#endif
-#ifndef JT_RAY_FROM_PATH
-#define JT_RAY_FROM_PATH 1
-#endif
+#include "jt_kernels.h"
 
 using namespace jtd;
+using namespace jtk;
 
-namespace {
+namespace jtk {
+// every configuration is compiled in its own translation unit (jt_kv.hip)
+JT_KV_FOR(0, extern template)
+JT_KV_FOR(1, extern template)
+JT_KV_FOR(2, extern template)
+JT_KV_FOR(3, extern template)
+JT_KV_FOR(4, extern template)
+JT_KV_FOR(5, extern template)
+JT_KV_FOR(6, extern template)
 
-// ============================================================================ scene evaluation
-__device__ __forceinline__ fr3 inst_frame(const DScene& S, int inst) {
-    const DInstShade& r = S.inst_shade[inst];
-    return frame_from(r.f0, r.f1, r.f2);
-}
-
-// eval_position (src/scene.jl:435-476)
-template <int F>
-__device__ __forceinline__ v3 eval_position(const DScene& S, int inst, int elem, v2 uv) {
-    const DInstShade& is = S.inst_shade[inst];
-    const DShape sh = S.shapes[is.shape];
-    const int4 e = S.elems[sh.idx_base + elem];
-    const fr3 f = frame_from(is.f0, is.f1, is.f2);
-    v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
-    if (!(F & FT_QUAD) || sh.kind == KIND_TRI) return transform_point(f, interp_tri(p1, p2, p3, uv));
-    return transform_point(f, interp_quad(p1, p2, p3, xyz(S.pos[e.w]), uv));
-}
-// eval_element_normal (src/scene.jl:578-612): transform_normal(frame, triangle/quad normal),
-// with the element normal (and, for an unrotated frame, the whole result) precomputed
-__device__ __forceinline__ v3 element_normal(const DScene& S, const DInstShade& is, const fr3& f, int g) {
-    if (is.rot_identity) return xyz(S.enrm_id[g]);
-    return transform_normal(f, xyz(S.enrm[g]));
-}
-__device__ __forceinline__ v3 eval_element_normal(const DScene& S, int inst, int elem) {
-    const DInstShade& is = S.inst_shade[inst];
-    const DShape sh = S.shapes[is.shape];
-    return element_normal(S, is, frame_from(is.f0, is.f1, is.f2), sh.idx_base + elem);
-}
-// eval_normal (src/scene.jl:525-576)
-__device__ __forceinline__ v3 eval_normal(const DScene& S, const DShape& sh, const int4& e, const fr3& f, v2 uv) {
-    if (sh.nrm_base < 0) {
-        v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
-        if (sh.kind == KIND_TRI) return transform_normal(f, triangle_normal(p1, p2, p3));
-        return transform_normal(f, quad_normal(p1, p2, p3, xyz(S.pos[e.w])));
-    }
-    const int b = sh.nrm_base - sh.pos_base;  // normals share vertex ids with positions
-    v3 n1 = xyz(S.nrm[e.x + b]), n2 = xyz(S.nrm[e.y + b]), n3 = xyz(S.nrm[e.z + b]);
-    if (sh.kind == KIND_TRI) return transform_normal(f, normalize(interp_tri(n1, n2, n3, uv)));
-    return transform_normal(f, normalize(interp_quad(n1, n2, n3, xyz(S.nrm[e.w + b]), uv)));
-}
-// eval_texcoord (src/scene.jl:753-788)
-__device__ __forceinline__ v2 eval_texcoord(const DScene& S, const DShape& sh, const int4& e, v2 uv) {
-    if (sh.tc_base < 0) return uv;
-    const int b = sh.tc_base - sh.pos_base;
-    float2 t1 = S.tc[e.x + b], t2 = S.tc[e.y + b], t3 = S.tc[e.z + b];
-    if (sh.kind == KIND_TRI) return interp_tri(V2(t1.x, t1.y), V2(t2.x, t2.y), V2(t3.x, t3.y), uv);
-    float2 t4 = S.tc[e.w + b];
-    return interp_quad(V2(t1.x, t1.y), V2(t2.x, t2.y), V2(t3.x, t3.y), V2(t4.x, t4.y), uv);
-}
-// eval_color (src/scene.jl:690-720)
-__device__ __forceinline__ v4 eval_color(const DScene& S, const DShape& sh, const int4& e, v2 uv) {
-    if (sh.col_base < 0) return V4(1, 1, 1, 1);
-    const int b = sh.col_base - sh.pos_base;
-    float4 c1 = S.col[e.x + b], c2 = S.col[e.y + b], c3 = S.col[e.z + b];
-    v4 a = V4(c1.x, c1.y, c1.z, c1.w), bb = V4(c2.x, c2.y, c2.z, c2.w), c = V4(c3.x, c3.y, c3.z, c3.w);
-    if (sh.kind == KIND_TRI) return interp_tri(a, bb, c, uv);
-    float4 c4 = S.col[e.w + b];
-    return interp_quad(a, bb, c, V4(c4.x, c4.y, c4.z, c4.w), uv);
-}
-// lookup_texture (src/scene.jl:836-849): 8-bit texels decode through exact host-built LUTs
-__device__ __forceinline__ v4 lookup_texture(const DScene& S, const DTexture& t, int i, int j, bool as_linear) {
-    long long k = t.offset + (long long)j * t.width + i;
-    if (t.is_float) {
-        float4 c = S.texf[k];
-        return V4(c.x, c.y, c.z, c.w);
-    }
-    uchar4 b = S.texb[k];
-    const float* lut = (as_linear && !t.linear) ? S.srgb_lut : S.byte_lut;
-    return V4(lut[b.x], lut[b.y], lut[b.z], S.byte_lut[b.w]);
-}
-// mod1(x, 1.0f0) (Julia base: mod via rem, then 0 -> 1)
-__device__ __forceinline__ float jl_mod1(float x) {
-    float r = __builtin_fmodf(x, 1.0f);
-    float m = r == 0 ? __builtin_copysignf(r, 1.0f) : (r < 0 ? r + 1.0f : r);
-    return m == 0 ? 1.0f : m;
-}
-// eval_texture (src/scene.jl:790-834): bilinear, wrap
-__device__ __forceinline__ v4 eval_texture(const DScene& S, int tex, v2 uv, bool as_linear) {
-    if (tex < 0) return V4(1, 1, 1, 1);
-    const DTexture t = S.textures[tex];
-    if (t.width == 0 || t.height == 0) return V4(0, 0, 0, 0);
-    float s = jl_mod1(uv.x) * (float)t.width;
-    if (s < 0) s += (float)t.width;
-    float tt = jl_mod1(uv.y) * (float)t.height;
-    if (tt < 0) tt += (float)t.height;
-    int i = jl_clampi((int)__builtin_truncf(s), 0, t.width - 1);
-    int j = jl_clampi((int)__builtin_truncf(tt), 0, t.height - 1);
-    int ii = (i + 1) % t.width, jj = (j + 1) % t.height;
-    float u = s - (float)i, v = tt - (float)j;
-    v4 a = (lookup_texture(S, t, i, j, as_linear) * (1 - u)) * (1 - v);
-    v4 b = (lookup_texture(S, t, i, jj, as_linear) * (1 - u)) * v;
-    v4 c = (lookup_texture(S, t, ii, j, as_linear) * u) * (1 - v);
-    v4 d = (lookup_texture(S, t, ii, jj, as_linear) * u) * v;
-    return ((a + b) + c) + d;
-}
-// eval_normalmap (src/scene.jl:722-751) with eval_element_tangents (:851-891)
-__device__ __forceinline__ v3 eval_normalmap(const DScene& S, const DShape& sh, const int4& e, const fr3& f,
-                                          const DMaterial& m, v2 uv) {
-    v3 normal = eval_normal(S, sh, e, f, uv);
-    v2 texcoord = eval_texcoord(S, sh, e, uv);
-    v4 t4 = eval_texture(S, m.normal_tex, texcoord, false);
-    v3 nm = V3(t4.x * 2 - 1, t4.y * 2 - 1, t4.z * 2 - 1);
-    v3 tu = V3(0, 0, 0), tv = V3(0, 0, 0);
-    if (sh.tc_base >= 0) {
-        const int b = sh.tc_base - sh.pos_base;
-        float2 a1 = S.tc[e.x + b], a2 = S.tc[e.y + b];
-        if (sh.kind == KIND_TRI) {
-            float2 a3 = S.tc[e.z + b];
-            triangle_tangents_fromuv(xyz(S.pos[e.x]), xyz(S.pos[e.y]), xyz(S.pos[e.z]), V2(a1.x, a1.y),
-                                     V2(a2.x, a2.y), V2(a3.x, a3.y), tu, tv);
-        } else {  // quad_tangents_fromuv at current_uv = (0, 0): triangle (p1, p2, p4)
-            float2 a4 = S.tc[e.w + b];
-            triangle_tangents_fromuv(xyz(S.pos[e.x]), xyz(S.pos[e.y]), xyz(S.pos[e.w]), V2(a1.x, a1.y),
-                                     V2(a2.x, a2.y), V2(a4.x, a4.y), tu, tv);
-        }
-        tu = transform_direction(f, tu);
-        tv = transform_direction(f, tv);
-    }
-    v3 f1 = normalize(tu - normal * dot(tu, normal));  // orthonormalize(frame[1], frame[3])
-    v3 f2 = normalize(cross(normal, tu));
-    bool flip_v = dot(f2, tv) < 0;
-    nm = V3(nm.x, nm.y * (flip_v ? 1.0f : -1.0f), nm.z);
-    fr3 fr{f1, f2, normal, V3(0, 0, 0)};
-    return transform_normal(fr, nm);
-}
-
-struct Shading {
-    v3 position, normal;
-    MatPoint mat;
-};
-
-// eval_shading_position + eval_shading_normal + eval_material (src/scene.jl:416-673)
-template <int F>
-__device__ __forceinline__ void eval_shading(const DScene& S, int inst, int elem, v2 uv, v3 outgoing, Shading& out) {
-    const DInstShade is = S.inst_shade[inst];
-    const DShape sh = S.shapes[is.shape];
-    const int4 e = S.elems[sh.idx_base + elem];
-    const fr3 f = frame_from(is.f0, is.f1, is.f2);
-    const DMaterial& m = S.materials[is.material];
-    v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
-    const bool tri = !(F & FT_QUAD) || sh.kind == KIND_TRI;
-    v3 p4 = !tri ? xyz(S.pos[e.w]) : p3;
-    // position
-    out.position = tri ? transform_point(f, interp_tri(p1, p2, p3, uv))
-                       : transform_point(f, interp_quad(p1, p2, p3, p4, uv));
-    // shading normal
-    const int mtype = (F & FT_MAT) ? m.type : (int)M_MATTE;
-    v3 normal;
-    if ((F & FT_TEX) && m.normal_tex >= 0) {
-        normal = eval_normalmap(S, sh, e, f, m, uv);
-    } else if (!(F & FT_ATTR) || sh.nrm_base < 0) {
-        normal = element_normal(S, is, f, sh.idx_base + elem);
-    } else {
-        normal = eval_normal(S, sh, e, f, uv);
-    }
-    if (mtype != M_REFRACTIVE) normal = dot(normal, outgoing) >= 0 ? normal : -normal;
-    out.normal = normal;
-    // material point
-    MatPoint& p = out.mat;
-    const v4 one = V4(1, 1, 1, 1);
-    v2 texcoord = (F & FT_ATTR) ? eval_texcoord(S, sh, e, uv) : uv;
-    v4 emission_tex = (F & FT_TEX) ? eval_texture(S, m.emission_tex, texcoord, true) : one;
-    v4 color_shp = (F & FT_ATTR) ? eval_color(S, sh, e, uv) : one;
-    v4 color_tex = (F & FT_TEX) ? eval_texture(S, m.color_tex, texcoord, true) : one;
-    v4 roughness_tex = (F & FT_TEX) ? eval_texture(S, m.roughness_tex, texcoord, false) : one;
-    v4 scattering_tex = (F & FT_TEX) ? eval_texture(S, m.scattering_tex, texcoord, true) : one;
-    p.type = mtype;
-    p.emission = V3(m.emission[0], m.emission[1], m.emission[2]) * xyz(emission_tex);
-    p.color = (V3(m.color[0], m.color[1], m.color[2]) * xyz(color_tex)) * xyz(color_shp);
-    p.opacity = m.opacity * color_tex.w * color_shp.w;
-    p.metallic = m.metallic * roughness_tex.z;
-    float roughness = m.roughness * roughness_tex.y;
-    roughness = roughness * roughness;
-    p.ior = m.ior;
-    p.scattering = V3(m.scattering[0], m.scattering[1], m.scattering[2]) * xyz(scattering_tex);
-    p.scanisotropy = m.scanisotropy;
-    p.trdepth = m.trdepth;
-    if ((F & FT_VOL) && (mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE)) {
-        p.density = V3(-jl_log(jl_clamp(p.color.x, 0.0001f, 1.0f)) / p.trdepth,
-                       -jl_log(jl_clamp(p.color.y, 0.0001f, 1.0f)) / p.trdepth,
-                       -jl_log(jl_clamp(p.color.z, 0.0001f, 1.0f)) / p.trdepth);
-    } else {
-        p.density = V3(0, 0, 0);
-    }
-    if (mtype == M_MATTE || mtype == M_GLTFPBR || mtype == M_GLOSSY) roughness = jl_clamp(roughness, min_roughness, 1.0f);
-    else if (mtype == M_VOLUMETRIC) roughness = 0.0f;
-    else if (roughness < min_roughness) roughness = 0.0f;
-    p.roughness = roughness;
-}
-
-// eval_environment (src/scene.jl:893-914)
-template <int F>
-__device__ __forceinline__ v3 eval_environment(const DScene& S, v3 direction) {
-    v3 emission = V3(0, 0, 0);
-    if (!(F & FT_ENV)) return emission;  // no environments: the sum is empty
-    for (int k = 0; k < S.nenvs; k++) {
-        const DEnv& env = S.envs[k];
-        v3 wl = transform_direction(frame_from(env.inv), direction);
-        v2 tc = V2(jl_atan2(wl.z, wl.x) / (2.0f * pif), jl_acos(jl_clamp(wl.y, -1.0f, 1.0f)) / pif);
-        if (tc.x < 0.0f) tc.x = tc.x + 1.0f;
-        v4 t = eval_texture(S, env.tex, tc, false);
-        emission = emission + V3(env.emission[0], env.emission[1], env.emission[2]) * xyz(t);
-    }
-    return emission;
-}
-
-// ============================================================================ traversal (src/bvh.jl)
-// Unified per-lane stack in LDS, entry = type << 30 | snap << 24 | index (24 bits; jt_create
-// checks the scene fits). snap (HBM mode): the query's hit count when a pre-tested child was
-// pushed (SNAP_NONE: not pre-tested). Layout stack[k * BLOCK + lane]:
-// every lane owns one bank (conflict-free ds_read/write_b32 whatever the per-lane depth).
-// The LDS part is a ring of RING entries; when a scene's bound exceeds it (OVF), the oldest
-// entries spill to a per-pixel HBM area and come back one at a time when popped.
-constexpr int BLOCK = 256;
-constexpr unsigned T_TLAS = 0u, T_INST = 1u, T_BLAS = 2u;
-constexpr unsigned IDX_MASK = (1u << 24) - 1;
-constexpr unsigned SNAP_NONE = 63u << 24;
-
-struct Hit {
-    int inst, elem;
-    float u, v, t;
-    bool hit;
-};
-struct Counters {
-    unsigned rays, light_queries, nodes, instances, prims, shades, paths;
-};
-
-// A resumable BVH query per lane, for intersect_scene_bvh (root = TLAS node 0) and
-// intersect_instance_bvh (root = one instance entry). node_step() / prim_step() do one unit of work: one
-// node (box test + push), one instance entry (ray to instance space), or ONE primitive test of
-// the current leaf (leaf cursor), so every step costs about the same whatever a lane is doing.
-// Visit order — children far-first per d[axis] sign, a TLAS leaf's instances in order, a BLAS
-// leaf's primitives in order before anything else is popped — is exactly the reference's, so
-// the closest hit and its tie-breaking (t == tmax replaces; only t > tmax rejects) match.
-struct Trav {
-    v3 wo, wd, wdinv;  // world-space ray of the query
-    v3 lo, ld, ldinv;  // the ray every node test uses: the world ray, or inside a BLAS the ray
-                       // in the current instance's space (transform_ray, src/geometry.jl:107)
-    float tmax;
-    int sp;            // stack entries (all levels)
-    int low;           // OVF: entries [low, sp) are in the LDS ring, [0, low) in HBM
-    int inst_space;    // lo/ld/ldinv hold an instance-space ray (restore before a TLAS pop)
-    int negmask;       // bit a set <=> ld[a] < 0 (the push order of src/bvh.jl:331-341, 424-434)
-    int cur_inst, cur_kind;
-    int prim, nprim;   // leaf cursor: next primitive record, primitives left
-    int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
-    float h_u, h_v;
-    int nh;              // hits accepted so far (every tmax change), saturating at 63
-};
-
-__device__ __forceinline__ int neg_mask(v3 d) { return (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0); }
-
-__device__ __forceinline__ void world_ray(Trav& T) {
-    T.lo = T.wo;
-    T.ld = T.wd;
-    T.ldinv = T.wdinv;
-    T.negmask = neg_mask(T.wd);
-    T.inst_space = 0;
-}
-
-__device__ __forceinline__ Hit query_hit(const Trav& T) {
-    return Hit{T.h_inst, T.h_elem, T.h_u, T.h_v, T.tmax, T.h_inst >= 0};
-}
-
-__device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T.nprim > 0; }
-
-__device__ __forceinline__ void query_begin(Trav& T, v3 o, v3 d, unsigned root, int* stack) {
-    T.wo = o;
-    T.wd = d;
-    T.wdinv = V3(jl_rcp(d.x), jl_rcp(d.y), jl_rcp(d.z));  // ray_dinv (src/bvh.jl:322), no guard
-    T.lo = o;
-    T.ld = d;
-    T.ldinv = T.wdinv;
-    T.tmax = __builtin_inff();
-    T.nh = 0;
-    T.h_inst = -1;
-    T.h_elem = -1;
-    T.h_u = 0;
-    T.h_v = 0;
-    T.nprim = 0;
-    T.prim = 0;
-    T.cur_inst = -1;
-    T.cur_kind = KIND_TRI;
-    T.inst_space = 0;
-    T.negmask = neg_mask(d);
-    stack[0] = (int)root;
-    T.sp = 1;
-    T.low = 0;
-}
-
-// The current BLAS leaf's next primitive(s), in order (src/bvh.jl:444-484). Triangles go in
-// pairs: both tests are computed side by side (the record after the leaf's last one exists: the
-// array is padded), then accepted in order, the second against the tmax the first left. A
-// second pair runs in the same step when some lane's leaf has more than two left.
-// Triangle k of the current leaf and the next one come from one 80-B pair record (host layout:
-// the two triangles' components interleaved, 5 loads instead of 6 for two separate records).
-// k is 0 or 2.
-template <int F>
-__device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
-    const float4* r = S.prims + 5 * (T.prim + (k >> 1));
-    const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
-    const PrimHit p1 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.x, r0.z, r1.x), V3(r1.z, r2.x, r2.z),
-                                              V3(r3.x, r3.z, r4.x));
-    const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.y, r0.w, r1.y), V3(r1.w, r2.y, r2.w),
-                                              V3(r3.y, r3.w, r4.y));
-    if (tri_hit_before(p1, T.tmax)) {
-        T.nh += T.nh < 63 ? 1 : 0;
-        T.h_inst = T.cur_inst;
-        T.h_elem = __float_as_int(r4.z);
-        T.h_u = p1.u;
-        T.h_v = p1.v;
-        T.tmax = p1.t;
-    }
-    if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax)) {
-        T.nh += T.nh < 63 ? 1 : 0;
-        T.h_inst = T.cur_inst;
-        T.h_elem = __float_as_int(r4.w);
-        T.h_u = p2.u;
-        T.h_v = p2.v;
-        T.tmax = p2.t;
-    }
-}
-template <int COUNT, int F>
-__device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cnt) {
-    if (!(F & FT_QUAD) || T.cur_kind == KIND_TRI) {
-        tri_pair<F>(S, T, 0);
-        const bool more = T.nprim > 2;
-        if (__builtin_amdgcn_ballot_w64(more)) {
-            if (more) tri_pair<F>(S, T, 2);
-        }
-        const int n = T.nprim < 4 ? T.nprim : 4;
-        if (COUNT) cnt.prims += n;
-        T.prim += 2;  // pair records (only read again when the leaf had more than four)
-        T.nprim -= n;
-        return;
-    }
-    if (COUNT) cnt.prims++;
-    const float4* r = S.prims + 4 * T.prim;
-    const float4 a = r[0], b = r[1], c = r[2], d = r[3];
-    const PrimHit p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
-    if (p.hit) {
-        T.nh += T.nh < 63 ? 1 : 0;
-        T.h_inst = T.cur_inst;
-        T.h_elem = __float_as_int(a.w);
-        T.h_u = p.u;
-        T.h_v = p.v;
-        T.tmax = p.t;
-    }
-    T.prim += 1;
-    T.nprim -= 1;
-}
-
-template <int RING, bool OVF>
-__device__ __forceinline__ void st_push(const DScene& S, Trav& T, int* stack, int pixel, unsigned e) {
-    if (OVF) {
-        if (T.sp - T.low == S.ring) {  // ring full: the oldest entry moves to HBM
-            S.ovf[(size_t)pixel * S.ovf_stride + T.low] = stack[(T.low & (S.ring - 1)) * BLOCK];
-            T.low += 1;
-        }
-        stack[(T.sp & (S.ring - 1)) * BLOCK] = (int)e;
-    } else {
-        stack[T.sp * BLOCK] = (int)e;
-    }
-    T.sp += 1;
-}
-template <int RING, bool OVF>
-__device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* stack, int pixel) {
-    T.sp -= 1;
-    if (OVF) {
-        // the ring slot is read unconditionally (its address is always valid; a relaxed atomic
-        // load, which the compiler cannot merge with the HBM load) and the HBM entry only below
-        // the ring: written as a choice of the two addresses, the compiler made every pop one
-        // flat load waiting on both memory counters
-        const unsigned r = (unsigned)__hip_atomic_load(stack + (T.sp & (S.ring - 1)) * BLOCK, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (T.sp < T.low) {  // below the ring: this entry was spilled
-            T.low = T.sp;
-            return (unsigned)S.ovf[(size_t)pixel * S.ovf_stride + T.sp];
-        }
-        return r;
-    }
-    return (unsigned)stack[T.sp * BLOCK];
-}
-
-// Pop one stack entry: an instance entry or a TLAS/BLAS node. An instance visit and the box
-// test of its BLAS root are one step: the reference's instance visit pushes nothing but the
-// root (src/bvh.jl:345-351, 502-506), which is then the very next pop, so testing it in the same
-// step visits the same nodes in the same order.
-template <int RING, bool OVF, int COUNT, bool NCACHE, int F>
-__device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
-    // without FT_XFORM every instance ray is the world ray: no transform, no space switch
-    constexpr bool XF = (F & FT_XFORM) != 0;
-    const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
-    unsigned type = e >> 30, idx = e & IDX_MASK;
-    if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
-        if (COUNT) cnt.instances++;
-        const int4 ib = S.inst_blas[idx];  // blas_root, kind, identity, shape
-        if (!XF || ib.z) {
-            // inverse(identity) is exactly the identity: transform_ray returns the ray bit for bit
-            if (XF && T.inst_space) world_ray(T);
-        } else {
-            const DInstTrav it = S.inst_trav[idx];
-            const fr3 inv = frame_from(it.i0, it.i1, it.i2);
-            T.lo = transform_point(inv, T.wo);
-            T.ld = transform_vector(inv, T.wd);
-            T.ldinv = V3(jl_rcp(T.ld.x), jl_rcp(T.ld.y), jl_rcp(T.ld.z));
-            T.negmask = neg_mask(T.ld);
-            T.inst_space = 1;
-        }
-        T.cur_inst = (int)idx;
-        T.cur_kind = ib.y;
-        type = T_BLAS;
-        idx = (unsigned)ib.x;
-    } else if (XF && type == T_TLAS && T.inst_space) {
-        world_ray(T);  // back from an instance: TLAS nodes test the world ray
-    }
-    const bool blas = type == T_BLAS;
-    if (COUNT) cnt.nodes++;
-    // HBM mode: a child pre-tested at its parent with the tmax it still has (no hit since: its
-    // snapshot equals the hit count) passes this pop's box test too — same ray, same box, same
-    // tmax — so only its start/meta half is loaded
-    const unsigned snap = (e >> 24) & 63u;
-    float4 nb;
-    if (NCACHE && snap != 63u && snap == (unsigned)T.nh) {
-        nb = S.nodes[idx].b;
-    } else {
-        const DNode nd = S.nodes[idx];
-        if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
-        nb = nd.b;
-    }
-    const unsigned meta = __float_as_uint(nb.w);
-    const int start = __float_as_int(nb.z);
-    const int num = (int)(meta & 0xffffu);
-    if (meta >> 24) {  // internal: for d[axis] >= 0 push start, start+1 (start+1 pops first)
-        const int axis = (int)((meta >> 16) & 0xffu);
-        const bool neg = (T.negmask >> axis) & 1;  // d[axis] < 0
-        const unsigned tag = type << 30 | SNAP_NONE;
-        const unsigned c_far = (unsigned)(neg ? start + 1 : start), c_near = (unsigned)(neg ? start : start + 1);
-        if (JT_CHILD_PRETEST && NCACHE) {
-            // HBM mode: test both children (one 64-B pair) when their parent is visited. A child
-            // whose box fails now fails when popped too (the slab test is monotone in tmax, which
-            // only shrinks): count its pop and skip the push. A pushed child is tested again when
-            // popped, with that moment's tmax, exactly as the reference does. (+10 % bathroom1,
-            // +14 % ecosys; in LDS mode the extra tests cost more than the pops they save.)
-            const DNode n0 = S.nodes[c_far];
-            const DNode n1 = S.nodes[c_near];
-            const bool k0 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n0.a, n0.b);
-            const bool k1 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n1.a, n1.b);
-            if (COUNT) cnt.nodes += (k0 ? 0 : 1) + (k1 ? 0 : 1);
-            const unsigned ptag = type << 30 | (unsigned)T.nh << 24;  // pre-tested at hit count nh
-            if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_far);
-            if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_near);
-        } else {
-            st_push<RING, OVF>(S, T, stack, pixel, tag | c_far);
-            st_push<RING, OVF>(S, T, stack, pixel, tag | c_near);
-        }
-    } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
-        for (int k = num - 1; k >= 0; k--)
-            st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | SNAP_NONE | (unsigned)S.tlas_prims[start + k]);
-    } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
-        T.prim = start;
-        T.nprim = num;
-    }
-}
-
-// ============================================================================ lights (src/trace.jl)
-// sample_lights (src/trace.jl:968-1008)
-template <int F>
-__device__ __forceinline__ v3 sample_lights(const DScene& S, v3 position, float rl, float rel, v2 ruv) {
-    const int light_id = sample_uniform(S.nlights, rl);
-    const DLight l = S.lights[light_id - 1];
-    const float* cdf = S.cdf + l.cdf_offset;
-    if (l.instance >= 0) {
-        const int element = l.nguide ? sample_discrete_guided(cdf, l.ncdf, rel, S.guide_t + l.guide_offset,
-                                                              S.guide_a + l.guide_offset, l.nguide, l.guide_scale)
-                                     : sample_discrete(cdf, l.ncdf, rel);
-        const DShape sh = S.shapes[S.inst_shade[l.instance].shape];
-        v2 uv = (!(F & FT_QUAD) || sh.kind == KIND_TRI) ? sample_triangle(ruv) : ruv;
-        v3 lposition = eval_position<F>(S, l.instance, element - 1, uv);
-        return normalize(lposition - position);
-    }
-    if ((F & FT_ENV) && l.environment >= 0) {
-        const DEnv& env = S.envs[l.environment];
-        const DTexture t = S.textures[env.tex];
-        int idx;  // 1-based, used as-is (:990-993)
-        if (l.alias_offset >= 0) {
-            // alias-table variant (JT_ENV_ALIAS=1): O(1) — column from rel,
-            // keep-or-alias coin from ruv.x (an environment sample does not use ruv). It samples
-            // the pmf the CDF holds, so env_light_pdf is unchanged, but it maps random numbers to
-            // texels differently from upper_bound: statistically equal, not bit-exact.
-            const int col = jl_clampi((int)(rel * (float)l.ncdf), 0, l.ncdf - 1);
-            const float2 a = S.alias[l.alias_offset + col];
-            idx = (ruv.x < a.x ? col : __float_as_int(a.y)) + 1;
-        } else {
-            idx = l.nguide ? sample_discrete_guided(cdf, l.ncdf, rel, S.guide_t + l.guide_offset,
-                                                    S.guide_a + l.guide_offset, l.nguide, l.guide_scale)
-                           : sample_discrete(cdf, l.ncdf, rel);
-        }
-        float u = ((float)(idx % t.width) + 0.5f) / (float)t.width;
-        float v = (float)((((double)idx / (double)t.width) + 0.5) / (double)t.height);
-        float su, cu, sv, cv;
-        jl_sincos(u * 2 * pif, &su, &cu);
-        jl_sincos(v * pif, &sv, &cv);
-        return transform_direction(frame_from(env.frame), V3(cu * sv, cv, su * sv));
-    }
-    return V3(0, 0, 0);
-}
-// env-light term of sample_lights_pdf (src/trace.jl:1045-1079)
-__device__ __forceinline__ float env_light_pdf(const DScene& S, const DLight l, v3 direction) {
-    const float* cdf = S.cdf + l.cdf_offset;
-    const DEnv& env = S.envs[l.environment];
-    const DTexture t = S.textures[env.tex];
-    v3 wl = transform_direction(frame_from(env.inv), direction);
-    v2 tc = V2(jl_atan2(wl.z, wl.x) / (2 * pif), jl_acos(jl_clamp(wl.y, -1.0f, 1.0f)) / pif);
-    if (tc.x < 0) tc.x = tc.x + 1;
-    int i = jl_clampi((int)__builtin_truncf(tc.x * (float)t.width), 0, t.width - 1);
-    int j = jl_clampi((int)__builtin_truncf(tc.y * (float)t.height), 0, t.height - 1);
-    float prob = sample_discrete_pdf(cdf, j * t.width + i + 1) / cdf[l.ncdf - 1];
-    float angle = (2 * pif / (float)t.width) * (pif / (float)t.height) *
-                  jl_sin(pif * ((float)j + 0.5f) / (float)t.height);
-    return prob / angle;
-}
-
-// ============================================================================ integrator
-// trace_path / trace_naive restated as a per-lane state machine. Every iteration of the
-// kernel's shading phase issues exactly one BVH query per waiting lane — a closest-hit scene
-// query (PH_SCENE) or one intersect_instance_bvh query of sample_lights_pdf (PH_LIGHT) —
-// which the traversal phase then advances (node_step / prim_step). Float operations and RNG draws happen
-// in exactly the reference's order; only where the lane waits between them changes.
-enum : int { PH_SCENE = 0, PH_LIGHT = 1, PH_FINISH = 2 };  // PH_FINISH: path done, sample not yet accumulated
-enum : int { F_HIT = 1, F_VOLUME = 2 };
-
-struct Path {
-    v3 o, d;                    // pending ray (during PH_LIGHT the light query's: origin / incoming)
-    v3 radiance, weight;  // during PH_LIGHT weight already holds weight .* f (src/trace.jl:386)
-    Rng rng;
-    int bounce, opbounce, flags, phase;
-    float max_roughness;
-    // sample_lights_pdf in flight (src/trace.jl:1010-1084)
-    int li, lcount;
-    v3 lq;       // during PH_LIGHT: the shading position (st.o holds the light query's origin,
-                 // next_position of src/trace.jl:1039, so every query's ray is (st.o, st.d))
-    float pb;    // sample_bsdfcos_pdf / sample_scattering_pdf
-    float pdf, lpdf;
-    Volume vol;  // volume_stack[1] (the stack never holds more than one entry)
-};
-
-// while bounce < params.bounces: bounce += 1 (src/trace.jl:295-297, 487-489)
-__device__ __forceinline__ bool next_bounce(const DParams& P, Path& st) {
-    if (st.bounce >= P.bounces) return true;
-    st.bounce += 1;
-    st.phase = PH_SCENE;
-    return false;
-}
-// end of a bounce: weight checks and Russian roulette (src/trace.jl:455-465, 557-567)
-__device__ __forceinline__ bool after_weight(const DParams& P, Path& st) {
-    if (is_zero(st.weight) || !all_finite(st.weight)) return true;
-    if (st.bounce > 3) {
-        float rr_prob = jl_min(0.99f, max3(st.weight));
-        if (rand1f(st.rng) >= rr_prob) return true;
-        st.weight = st.weight * (1 / rr_prob);
-    }
-    return next_bounce(P, st);
-}
-// walk the light list: environment terms are added in place, an instance light starts its
-// query chain; after the last light the one-sample MIS weight is applied (src/trace.jl:386-397)
-template <int F>
-__device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P, Path& st) {
-    for (;;) {
-        st.li += 1;
-        if (st.li >= S.nlights) {
-            st.o = st.lq;  // the next bounce's ray starts at the shading position
-            const float pdf = st.pdf * sample_uniform_pdf(S.nlights);
-            st.weight = st.weight / (0.5f * st.pb + 0.5f * pdf);  // (weight .* f) / (...)
-            return after_weight(P, st);
-        }
-        const DLight l = S.lights[st.li];
-        if (l.instance >= 0) {
-            st.lpdf = 0.0f;
-            st.lcount = 0;
-            st.o = st.lq;  // the first query starts at the shading position
-            st.phase = PH_LIGHT;
-            return false;
-        }
-        if ((F & FT_ENV) && l.environment >= 0) st.pdf += env_light_pdf(S, l, st.d);
-    }
-}
-template <int F>
-__device__ __forceinline__ bool begin_light_pdf(const DScene& S, const DParams& P, Path& st) {
-    st.pdf = 0.0f;
-    st.li = -1;
-    st.lq = st.o;
-    return light_advance<F>(S, P, st);
-}
-// one intersect_instance_bvh result of the instance-light loop (src/trace.jl:1024-1044)
-template <int F>
-__device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Path& st, const Hit& h) {
-    if (h.hit) {
-        const DLight l = S.lights[st.li];
-        v3 lposition = eval_position<F>(S, l.instance, h.elem, V2(h.u, h.v));
-        v3 lnormal = eval_element_normal(S, l.instance, h.elem);
-        const float area = S.cdf[l.cdf_offset + l.ncdf - 1];
-        v3 dd = lposition - st.lq;
-        st.lpdf += dot(dd, dd) / (__builtin_fabsf(dot(lnormal, st.d)) * area);
-        st.o = lposition + st.d * 0.001f;
-        if (++st.lcount < 100) return false;
-    }
-    st.pdf += st.lpdf;
-    return light_advance<F>(S, P, st);
-}
-
-// trace_path's bounce body after the closest-hit query (src/trace.jl:298-453)
-// The albedo/normal running means (src/trace.jl:635-636) are updated as soon as the bounce-0
-// surface is accepted — their targets are final at that point — so they are not path state.
-// Per-lane running means of the lane's pixel, kept in LDS for the whole launch (a lane owns
-// its pixel for all its samples): acc[k * BLOCK], k = 0..3 image rgba, 4..6 albedo, 7..9
-// normal, 10 hit count of this launch (int). Loaded from / stored to HBM once per launch; the
-// per-sample lerps are the same float operations as a read-modify-write of the HBM buffers.
-// JT_LANE_LDS: 11 the lane's current sample (int), 12 its running-mean weight 1/(n+1) — per-sample
-// state parked in LDS instead of registers kept live (and spilled) across the traversal loop.
-#ifndef JT_LANE_LDS
-#define JT_LANE_LDS 1
-#endif
-// The mesh kernels gain (features2 +7 %, bathroom1 +1 %, ecosys +0.6 %). The FT_NONE kernels
-// keep only the sample index (12 slots, the weight is recomputed from it): with 13 slots
-// cornellbox's LDS-mode kernel no longer fit 5 workgroups per CU (-9 %); with 12 it does, and
-// its spills drop from 37 to 23 VGPRs (scratch 112 -> 80 B/lane, spill write-back 36.3 -> 22.6
-// GB per launch, +0.5 %; gpurun_out/ab_ll, s8).
-#ifndef JT_LANE_LDS_NONE
-#define JT_LANE_LDS_NONE 1
-#endif
-__host__ __device__ constexpr bool lane_lds(int F) { return JT_LANE_LDS && (F != FT_NONE || JT_LANE_LDS_NONE); }
-constexpr int ACC_SLOTS = JT_LANE_LDS ? 13 : 11;  // the host sizes LDS for the larger layout
-// Lane-LDS slots: [11] the lane's sample index, [12] its running-mean weight. The FT_NONE
-// kernels (JT_LANE_LDS_NONE) recompute the weight from the sample index instead of storing it:
-// with 12 slots cornellbox's LDS-mode workgroup still fits 5 per CU.
-__host__ __device__ constexpr int acc_slots(int F) { return lane_lds(F) ? (F == FT_NONE ? 12 : 13) : 11; }
-struct Aov {
-    float* acc;
-    float w_;    // !lane_lds(F)
-    int first_;  // params.first (the weight's sample offset)
-    template <int F>
-    __device__ __forceinline__ float w() const {
-        if (!lane_lds(F)) return w_;
-        if (F == FT_NONE) return 1.0f / (float)(reinterpret_cast<const int*>(acc)[11 * BLOCK] - first_ + 1);
-        return acc[12 * BLOCK];
-    }
-};
-template <int F>
-__device__ __forceinline__ void aov_update(const Aov& a, v3 ta, v3 tn) {
-    const float aw = a.w<F>();
-    const float omw = 1 - aw;
-    float* p = a.acc;
-    p[4 * BLOCK] = p[4 * BLOCK] * omw + ta.x * aw;
-    p[5 * BLOCK] = p[5 * BLOCK] * omw + ta.y * aw;
-    p[6 * BLOCK] = p[6 * BLOCK] * omw + ta.z * aw;
-    p[7 * BLOCK] = p[7 * BLOCK] * omw + tn.x * aw;
-    p[8 * BLOCK] = p[8 * BLOCK] * omw + tn.y * aw;
-    p[9 * BLOCK] = p[9 * BLOCK] * omw + tn.z * aw;
-}
-
-template <int F, class AovT>
-__device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const AovT& aov,
-                                         unsigned& shades) {
-    if (!isec.hit) {
-        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
-        return true;
-    }
-    bool in_volume = false;
-    if ((F & FT_VOL) && (st.flags & F_VOLUME)) {  // :307-326 (volumes need a volume material)
-        float rl = rand1f(st.rng), rd = rand1f(st.rng);
-        float distance = sample_transmittance(st.vol.density, isec.t, rl, rd);
-        v3 tr = eval_transmittance(st.vol.density, distance);
-        float tp = sample_transmittance_pdf(st.vol.density, distance, isec.t);
-        st.weight = (st.weight * tr) / tp;
-        in_volume = distance < isec.t;
-        isec.t = distance;
-    }
-    if (!in_volume) {  // surface (:328-423)
-        v3 outgoing = -st.d;
-        Shading sh;
-        eval_shading<F>(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
-        shades++;
-        if (P.nocaustics) {
-            st.max_roughness = jl_max(sh.mat.roughness, st.max_roughness);
-            sh.mat.roughness = st.max_roughness;
-        }
-        if ((F & FT_OPAC) && sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
-            if (st.opbounce > 128) return true;
-            st.opbounce += 1;
-            st.o = sh.position + st.d * 0.01f;
-            st.bounce -= 1;
-            return next_bounce(P, st);
-        }
-        if (st.bounce == 0) {
-            st.flags |= F_HIT;
-            aov_update<F>(aov, sh.mat.color, sh.normal);
-        }
-        st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
-        v3 incoming;
-        const bool delta = is_delta(sh.mat);
-        if (!delta) {
-            if (rand1f(st.rng) < 0.5f) {
-                float rnl = rand1f(st.rng);
-                v2 rn = rand2f(st.rng);
-                incoming = sample_bsdfcos<F>(sh.mat, sh.normal, outgoing, rnl, rn);
-            } else {
-                float rl = rand1f(st.rng), rel = rand1f(st.rng);
-                v2 ruv = rand2f(st.rng);
-                incoming = sample_lights<F>(S, sh.position, rl, rel, ruv);
-            }
-            if (is_zero(incoming)) return true;
-            st.weight = st.weight * eval_bsdfcos<F>(sh.mat, sh.normal, outgoing, incoming);
-            st.pb = sample_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
-        } else {
-            float rnl = rand1f(st.rng);
-            incoming = sample_delta<F>(sh.mat, sh.normal, outgoing, rnl);
-            v3 f = eval_delta<F>(sh.mat, sh.normal, outgoing, incoming);
-            float pd = sample_delta_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
-            st.weight = (st.weight * f) / pd;
-        }
-        // volume stack push/pop (:405-421); independent of the weight update it follows
-        const int mtype = sh.mat.type;
-        if ((F & FT_VOL) && (mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE) &&
-            dot(sh.normal, outgoing) * dot(sh.normal, incoming) < 0) {
-            if (!(st.flags & F_VOLUME)) {
-                st.flags |= F_VOLUME;  // eval_material again: only the volume fields are kept
-                st.vol.density = sh.mat.density;
-                st.vol.scattering = sh.mat.scattering;
-                st.vol.scanisotropy = sh.mat.scanisotropy;
-            } else {
-                st.flags &= ~F_VOLUME;
-            }
-        }
-        st.o = sh.position;
-        st.d = incoming;
-        return delta ? after_weight(P, st) : begin_light_pdf<F>(S, P, st);
-    }
-    // volume scattering (:424-453)
-    v3 outgoing = -st.d;
-    v3 position = st.o + st.d * isec.t;
-    v3 incoming;
-    if (rand1f(st.rng) < 0.5f) {
-        (void)rand1f(st.rng);  // rnl: drawn, unused by sample_scattering
-        v2 rn = rand2f(st.rng);
-        incoming = sample_scattering(st.vol, outgoing, rn);
-    } else {
-        float rl = rand1f(st.rng), rel = rand1f(st.rng);
-        v2 ruv = rand2f(st.rng);
-        incoming = sample_lights<F>(S, position, rl, rel, ruv);
-    }
-    if (is_zero(incoming)) return true;
-    st.weight = st.weight * eval_scattering(st.vol, outgoing, incoming);
-    st.pb = sample_scattering_pdf(st.vol, outgoing, incoming);
-    st.o = position;
-    st.d = incoming;
-    return begin_light_pdf<F>(S, P, st);
-}
-
-// trace_naive's bounce body after the closest-hit query (src/trace.jl:490-569)
-template <int F, class AovT>
-__device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const AovT& aov,
-                                          unsigned& shades) {
-    if (!isec.hit) {
-        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
-        return true;
-    }
-    v3 outgoing = -st.d;
-    Shading sh;
-    eval_shading<F>(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
-    shades++;
-    if ((F & FT_OPAC) && sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
-        if (st.opbounce > 128) return true;
-        st.opbounce += 1;
-        st.o = sh.position + st.d * 0.01f;
-        st.bounce -= 1;
-        return next_bounce(P, st);
-    }
-    if (st.bounce == 0) {
-        st.flags |= F_HIT;
-        aov_update<F>(aov, sh.mat.color, sh.normal);
-    }
-    st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
-    v3 incoming, f;
-    float p;
-    if (sh.mat.roughness != 0) {
-        float rnl = rand1f(st.rng);
-        v2 rn = rand2f(st.rng);
-        incoming = sample_bsdfcos<F>(sh.mat, sh.normal, outgoing, rnl, rn);
-        if (is_zero(incoming)) return true;
-        f = eval_bsdfcos<F>(sh.mat, sh.normal, outgoing, incoming);
-        p = sample_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
-    } else {
-        float rnl = rand1f(st.rng);
-        incoming = sample_delta<F>(sh.mat, sh.normal, outgoing, rnl);
-        if (is_zero(incoming)) return true;
-        f = eval_delta<F>(sh.mat, sh.normal, outgoing, incoming);
-        p = sample_delta_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
-    }
-    st.weight = (st.weight * f) / p;
-    st.o = sh.position;
-    st.d = incoming;
-    return after_weight(P, st);
-}
-
-// eval_camera (src/scene.jl:372-411)
-__device__ __forceinline__ void eval_camera(const DCamera& cam, v2 image_uv, v2 lens_uv, v3& ro, v3& rd) {
-    const fr3 frame = frame_from(cam.frame);
-    const v2 film = V2(cam.film_x, cam.film_y);
-    if (!cam.orthographic) {
-        v3 q = V3(film.x * (0.5f - image_uv.x), film.y * (image_uv.y - 0.5f), cam.lens);
-        v3 dc = -normalize(q);
-        v3 e = V3(lens_uv.x * cam.aperture / 2, lens_uv.y * cam.aperture / 2, 0);
-        v3 p = (dc * cam.focus) / __builtin_fabsf(dc.z);
-        v3 d = normalize(p - e);
-        ro = transform_point(frame, e);
-        rd = transform_direction(frame, d);
-    } else {
-        float scale = 1 / cam.lens;
-        v3 q = V3(film.x * (0.5f - image_uv.x) * scale, film.y * (image_uv.y - 0.5f) * scale, cam.lens);
-        v3 e = V3(-q.x, -q.y, 0) + V3(lens_uv.x * cam.aperture / 2, lens_uv.y * cam.aperture / 2, 0);
-        v3 p = V3(-q.x, -q.y, -cam.focus);
-        v3 d = normalize(p - e);
-        ro = transform_point(frame, e);
-        rd = transform_direction(frame, d);
-    }
-}
-
-// trace_sample prologue (src/trace.jl:597-608): 4 draws, camera ray (sample_camera :651-674)
-__device__ __forceinline__ void start_path(const DParams& P, int i, int j, int pixel, int sample, Path& st) {
-    st.rng = rng_init(P.seed, pixel, sample);
-    v2 puv = rand2f(st.rng);
-    v2 luv = rand2f(st.rng);
-    v2 uv;
-    if (!P.tentfilter) {
-        uv = V2(((float)i + puv.x) / (float)P.width, ((float)j + puv.y) / (float)P.height);
-    } else {
-        const float width = 2.0f, offset = 0.5f;
-        v2 fuv = V2(width * (puv.x < 0.5f ? __builtin_sqrtf(2 * puv.x) - 1 : 1 - __builtin_sqrtf(2 - 2 * puv.x)) + offset,
-                    width * (puv.y < 0.5f ? __builtin_sqrtf(2 * puv.y) - 1 : 1 - __builtin_sqrtf(2 - 2 * puv.y)) + offset);
-        uv = V2(((float)i + fuv.x) / (float)P.width, ((float)j + fuv.y) / (float)P.height);
-    }
-    eval_camera(P.cam, uv, P.cam.pinhole ? sample_disk_signs(luv) : sample_disk(luv), st.o, st.d);
-    st.radiance = V3(0, 0, 0);
-    st.weight = V3(1, 1, 1);
-    st.max_roughness = 0.0f;
-    st.bounce = 0;  // the first loop iteration: bounce = -1 + 1 (bounces >= 0 always enters)
-    st.opbounce = 0;
-    st.flags = 0;
-    st.phase = PH_SCENE;
-}
-
-// active lanes of a ballot, as a 32-bit scalar (keeps the comparisons of counts on the SALU)
-__device__ __forceinline__ int lane_count(unsigned long long m) {
-    return __builtin_popcount((unsigned)m) + __builtin_popcount((unsigned)(m >> 32));
-}
-
-__device__ __forceinline__ unsigned wave_sum(unsigned v) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-struct DAccum {
-    float4* image;
-    float4* albedo;
-    float4* normal;
-    long long* hits;
-    unsigned long long* counters;  // 7 x u64: paths rays light_queries nodes instances prims shades;
-                                   // [7]: tile-order wait timeouts (must stay 0)
-    unsigned* work;                // unit counters of the launch, one per XCD band at work[16 b]
-                                   // (zeroed before each launch)
-    int* tile_done;                // per 8x8 tile: sample chunks accumulated in this launch
-};
-
-// Work units: (sample chunk c, 8x8 pixel tile t), fetched by whole waves from atomic counters,
-// so every wave stays busy until the launch's last units. The tiles are split into 8 bands of
-// rows, one per XCD: a wave drains its own XCD's band first (neighbouring pixels share that
-// XCD's L2), then helps the other bands. Within a band units are numbered chunk-major, and a
-// tile's chunks run in order: a wave takes (c, t) only after (c - 1, t) has published its
-// running means (agent-scope release/acquire: a helper may run on another XCD).
-constexpr int NBANDS = 8, BAND_STRIDE = 16;
-__device__ __forceinline__ void wait_tile(const DAccum& A, int t, int c) {
-    if ((threadIdx.x & 63) == 0) {
-        int n = 0;
-        while (__hip_atomic_load(A.tile_done + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c) {
-            __builtin_amdgcn_s_sleep(8);
-            if (++n > (1 << 27)) {  // never expected (units are fetched in order): flag, do not hang
-                atomicAdd(A.counters + 7, 1ull);
-                break;
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-__device__ __forceinline__ void publish_tile(const DAccum& A, int t, int c) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if ((threadIdx.x & 63) == 0) __hip_atomic_store(A.tile_done + t, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// sample range of chunk uc of a launch over [s_begin, s_end)
-__device__ __forceinline__ int num_chunks(const DParams& P, int s_begin, int s_end) {
-    return P.nct > 0 ? P.nct : (s_end - s_begin + P.chunk - 1) / P.chunk;
-}
-__device__ __forceinline__ void chunk_range(const DParams& P, int s_begin, int s_end, int uc, int& cs0, int& cs1) {
-    if (P.nct > 0) {
-        cs0 = s_begin + P.cbeg[uc];
-        cs1 = s_begin + P.cbeg[uc + 1];
-    } else {
-        cs0 = s_begin + uc * P.chunk;
-        cs1 = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
-    }
-}
-
-// lane id (0..63) recomputed where it is used: an asm the compiler cannot merge with an earlier one
-__device__ __forceinline__ int opaque_lane_id() {
-    unsigned l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return (int)l;
-}
-
-// trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
-// 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
-// mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE>
-__device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
-                                           int* stack) {
-    const int lane = threadIdx.x & 63;
-    Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    // WC: paths, scene rays and light queries are counted per wave (ballots at wave-uniform
-    // points, scalar registers), not per lane: three fewer VGPRs live across the traversal loop.
-    // The mesh kernels gain (bathroom1 +3 %, features2 +1 %); the FT_NONE kernel, whose light-hit
-    // steps run the ballots every few iterations, loses 1.5 % and keeps per-lane counters.
-    constexpr bool WC = F != FT_NONE;
-    unsigned w_paths = 0, w_rays = 0, w_lq = 0;
-    constexpr bool LL = lane_lds(F);
-    __shared__ float acc_lds[acc_slots(F) * BLOCK];
-    float* acc = acc_lds + threadIdx.x;
-#if JT_STAMPS
-    unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
-    unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
-    unsigned long long dead_lanes = 0;  // lanes done with their unit's samples, per traversal iteration
-#endif
-    const int tiles_x = (P.width + 7) / 8, tiles = tiles_x * ((P.height + 7) / 8);
-    const int nchunks = num_chunks(P, s_begin, s_end);
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    int band_k = 0;
-    for (;;) {
-    const int band = (int)((xcc + (unsigned)band_k) & (NBANDS - 1));
-    const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
-    unsigned unit = 0;
-    if (lane == 0) unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
-    unit = __builtin_amdgcn_readfirstlane(unit);
-    if (unit >= (unsigned)bn * (unsigned)nchunks) {  // this band is drained: help the next one
-        if (++band_k >= NBANDS) break;
-        continue;
-    }
-    const int uc = (int)(unit / (unsigned)bn), ut = bt0 + (int)(unit % (unsigned)bn);
-    if (uc > 0) wait_tile(A, ut, uc);
-    const int i = (ut % tiles_x) * 8 + (lane & 7);
-    const int j = (ut / tiles_x) * 8 + (lane >> 3);
-    int cs0, cs1;
-    chunk_range(P, s_begin, s_end, uc, cs0, cs1);
-    int pixel = j * P.width + i;
-    bool in_image = i < P.width && j < P.height;
-    bool alive = in_image;
-    int sample = cs0;
-    if (in_image) {
-        const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
-        acc[0] = im.x;
-        acc[BLOCK] = im.y;
-        acc[2 * BLOCK] = im.z;
-        acc[3 * BLOCK] = im.w;
-        acc[4 * BLOCK] = al.x;
-        acc[5 * BLOCK] = al.y;
-        acc[6 * BLOCK] = al.z;
-        acc[7 * BLOCK] = nr.x;
-        acc[8 * BLOCK] = nr.y;
-        acc[9 * BLOCK] = nr.z;
-        reinterpret_cast<int*>(acc)[10 * BLOCK] = 0;
-    }
-    int* const acc_i = reinterpret_cast<int*>(acc);
-    Aov aov{acc, 0.0f, P.first};
-    if (LL) {
-        if (in_image) {
-            acc_i[11 * BLOCK] = sample;
-            if (F != FT_NONE) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
-        }
-    } else {
-        aov.w_ = 1.0f / (float)(sample - P.first + 1);
-    }
-    Path st;
-    Trav T;
-    // lane states, from the stack cursor alone: sp < 0 finished (no samples left), nprim > 0 or
-    // sp > 0 in a query, sp == nprim == 0 waiting for the shading phase
-    T.sp = -1;
-    T.nprim = 0;
-    if (alive) {
-        start_path(P, i, j, pixel, sample, st);
-        query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
-    }
-    if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(alive));
-    else cnt.rays += alive ? 1 : 0;
-    for (;;) {
-#if JT_STAMPS
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
-        // traversal phase: step every lane with a query in flight until at least W lanes wait
-        // Each iteration runs ONE step kind — primitive tests or stack pops — picked by lane
-        // majority (a wave-uniform branch), so the SIMD executes one code path per iteration.
-        // A lane's own sequence of steps is unchanged: it only waits while the other kind runs.
-        // Light-hit steps (path sampler, scenes without environments, whose light_hit is short):
-        // a lane whose sample_lights_pdf query has finished does not wait for the shading
-        // phase — once enough such lanes gather (or nothing else is left to step) the wave runs
-        // light_hit on them and their next query starts at once.
-        constexpr bool LSTEP = SAMPLER == 1 && !(F & FT_ENV);
-        for (;;) {
-            const bool wantp = T.nprim > 0;
-            const bool wantn = T.nprim == 0 && T.sp > 0;
-            const bool waiting = (T.sp | T.nprim) == 0;
-            const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
-            const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
-            int nw = lane_count(__builtin_amdgcn_ballot_w64(waiting));
-            const int nb = np + nn;
-            if (LSTEP) {
-                const bool wantl = waiting && st.phase == PH_LIGHT;
-                const int nl = lane_count(__builtin_amdgcn_ballot_w64(wantl));
-                if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
-                    bool c_lq = false, c_ray = false;
-                    if (wantl) {
-                        if (light_hit<F>(S, P, st, query_hit(T))) {
-                            st.phase = PH_FINISH;
-                        } else if (st.phase == PH_LIGHT) {
-                            if (WC) c_lq = true;
-                            else cnt.light_queries++;
-                            query_begin(T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
-                        } else {
-                            if (WC) c_ray = true;
-                            else cnt.rays++;
-                            query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
-                        }
-                    }
-                    if (WC) {
-                        w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
-                        w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
-                    }
-                    continue;
-                }
-                nw -= nl;
-            }
-            if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
-#if JT_STAMPS
-            n_trav++;
-            dead_lanes += 64 - lane_count(__builtin_amdgcn_ballot_w64(T.sp >= 0));
-            if (np >= nn) { steps_p++; lanes_p += np; } else { steps_n++; lanes_n += nn; }
-#endif
-            if (JT_RAY_FROM_PATH && !(F & FT_XFORM)) {
-                // without instance transforms a query's ray is its path's (st.o, st.d), unchanged
-                // while the query runs: re-reading it here keeps one copy, not two, live across
-                // the loop (register renaming only, no instructions)
-                T.lo = st.o;
-                T.ld = st.d;
-            }
-            if (np >= nn) {
-                if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-            } else {
-                // JT_NODE_REPEAT pops per node iteration: a lane whose next step is again a
-                // stack pop takes it at once (the same steps in the same per-lane order, less
-                // per-iteration vote and loop overhead)
-                constexpr int NREP = F == FT_NONE ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
-#pragma unroll
-                for (int k = 0; k < NREP; k++)
-                    if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
-            }
-        }
-#if JT_STAMPS
-        unsigned long long t1 = __builtin_amdgcn_s_memtime();
-        t_trav += t1 - t0;
-        n_shade++;
-#endif
-        // shading phase: every waiting lane consumes its hit and issues its next query
-        bool c_path = false, c_lq = false, c_ray = false;
-        if ((T.sp | T.nprim) == 0) {
-            bool alive = true;
-            const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
-            bool done;
-#if JT_STAMPS
-            unsigned long long s0 = __builtin_amdgcn_s_memtime();
-            if (light) done = light_hit<F>(S, P, st, query_hit(T));
-            unsigned long long s1 = __builtin_amdgcn_s_memtime();
-            if (LSTEP && st.phase == PH_FINISH) done = true;
-            else if (!light) {
-                if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
-                else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
-            }
-            unsigned long long s2 = __builtin_amdgcn_s_memtime();
-            if (__ballot(light)) { t_lhit += s1 - s0; n_lhit++; }
-            if (__ballot(!light)) { t_phit += s2 - s1; n_phit++; }
-            if (__ballot(done)) n_fin++;
-#else
-            if (LSTEP && st.phase == PH_FINISH) done = true;
-            else if (light) done = light_hit<F>(S, P, st, query_hit(T));
-            else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
-            else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
-#endif
-            if (done) {
-                // trace_sample epilogue (src/trace.jl:625-648)
-                if (WC) c_path = true;
-                else cnt.paths++;
-                v3 radiance = st.radiance;
-                if (!all_finite(radiance)) radiance = V3(0, 0, 0);
-                const float mr = max3(radiance);
-                if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
-                const float w = aov.w<F>();
-                const float omw = 1 - w;
-                const bool hit = st.flags & F_HIT;
-                const bool env = !hit && !P.envhidden && S.nenvs != 0;
-                const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
-                // no bounce-0 surface was accepted: st.d is still the camera ray direction
-                if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
-                acc[0] = acc[0] * omw + target.x * w;
-                acc[BLOCK] = acc[BLOCK] * omw + target.y * w;
-                acc[2 * BLOCK] = acc[2 * BLOCK] * omw + target.z * w;
-                acc[3 * BLOCK] = acc[3 * BLOCK] * omw + target.w * w;
-                if (hit || env) reinterpret_cast<int*>(acc)[10 * BLOCK] += 1;
-                if constexpr (LL) {
-                // the pixel from the unit's wave-uniform tile and a lane id the compiler cannot
-                // reuse from the top of the unit, so i / j do not stay live across the loop
-                const int sample = acc_i[11 * BLOCK] + 1;
-                if (sample >= cs1) {
-                    alive = false;
-                    T.sp = -1;
-                } else {
-                    acc_i[11 * BLOCK] = sample;
-                    if (F != FT_NONE) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
-                    const int lx = opaque_lane_id();
-                    const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
-                    start_path(P, i2, j2, j2 * P.width + i2, sample, st);
-                }
-                } else {
-                if (++sample >= cs1) {
-                    alive = false;
-                    T.sp = -1;
-                } else {
-                    aov.w_ = 1.0f / (float)(sample - P.first + 1);
-                    start_path(P, i, j, pixel, sample, st);
-                }
-                }
-            }
-#if JT_STAMPS
-            unsigned long long s3 = __builtin_amdgcn_s_memtime();
-            t_fin += s3 - s2;
-#endif
-            if (alive) {
-                if (SAMPLER == 1 && st.phase == PH_LIGHT) {
-                    if (WC) c_lq = true;
-                    else cnt.light_queries++;
-                    query_begin(T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
-                } else {
-                    if (WC) c_ray = true;
-                    else cnt.rays++;
-                    query_begin(T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
-                }
-                // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
-                // where most of the wave's lanes take part, rather than in a sparser traversal step
-#pragma unroll
-                for (int k = 0; k < JT_FIRST_POP; k++)
-                    if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
-            }
-#if JT_STAMPS
-            t_qb += __builtin_amdgcn_s_memtime() - s3;
-#endif
-        }
-#if JT_STAMPS
-        t_shade += __builtin_amdgcn_s_memtime() - t1;
-#endif
-        if (WC) {
-            w_paths += lane_count(__builtin_amdgcn_ballot_w64(c_path));
-            w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
-            w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
-        }
-        if (__ballot(T.sp >= 0) == 0) break;
-    }
-    if constexpr (LL) {
-        const int lx = opaque_lane_id();
-        const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
-        pixel = j2 * P.width + i2;
-        in_image = i2 < P.width && j2 < P.height;
-    }
-    if (in_image) {
-        A.image[pixel] = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);
-        A.albedo[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
-        A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
-        A.hits[pixel] += reinterpret_cast<const int*>(acc)[10 * BLOCK];
-    }
-    if (uc + 1 < nchunks) publish_tile(A, ut, uc);
-    }  // units
-#if JT_STAMPS
-    if (lane == 0) {
-        unsigned long long* dbg = A.counters + 8;
-        atomicAdd(dbg + 0, t_trav);
-        atomicAdd(dbg + 1, t_shade);
-        atomicAdd(dbg + 2, n_trav);
-        atomicAdd(dbg + 3, n_shade);
-        atomicAdd(dbg + 4, lanes_p);
-        atomicAdd(dbg + 5, lanes_n);
-        atomicAdd(dbg + 6, steps_p);
-        atomicAdd(dbg + 7, steps_n);
-        atomicAdd(dbg + 8, t_lhit);
-        atomicAdd(dbg + 9, t_phit);
-        atomicAdd(dbg + 10, t_fin);
-        atomicAdd(dbg + 11, t_qb);
-        atomicAdd(dbg + 12, n_lhit);
-        atomicAdd(dbg + 13, n_phit);
-        atomicAdd(dbg + 14, n_fin);
-        atomicAdd(dbg + 15, dead_lanes);
-    }
-#endif
-    // one atomic per counter per wave
-    const unsigned wv[3] = {w_paths, w_rays, w_lq};
-    unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
-                     COUNT ? cnt.shades : 0u};
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-        unsigned s = (WC && k < 3) ? wv[k] : wave_sum(v[k]);
-        if (lane == 0 && s) atomicAdd(&A.counters[k], (unsigned long long)s);
-    }
-}
-
-// Occupancy request (waves per SIMD); JT_WAVES=0 leaves it to the compiler. The LDS-mode
-// FT_NONE kernel (cornellbox: 96 VGPRs, LDS for 5 workgroups per CU with the stack sized to the
-// scene) asks for JT_WAVES_NONE: measured +4 % over 4 waves with its wait_lanes of 56.
-#ifndef JT_WAVES
-#define JT_WAVES 0
-#endif
-#ifndef JT_WAVES_NONE
-#define JT_WAVES_NONE 5
-#endif
-#if JT_WAVES > 0
-#define JT_WAVES_PER_EU __attribute__((amdgpu_waves_per_eu(JT_WAVES, JT_WAVES)))
-#define JT_WAVES_PER_EU_F(F) \
-    __attribute__((amdgpu_waves_per_eu((F) == FT_NONE ? JT_WAVES_NONE : JT_WAVES, (F) == FT_NONE ? JT_WAVES_NONE : JT_WAVES)))
-#else
-#define JT_WAVES_PER_EU
-#define JT_WAVES_PER_EU_F(F)
-#endif
-// the scene arrays of the LDS blob (small-scene mode; offsets from jt_create)
-__device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob) {
-    DScene L = S;
-    L.nodes = reinterpret_cast<const DNode*>(blob + S.o_nodes);
-    L.tlas_prims = reinterpret_cast<const int*>(blob + S.o_tlas_prims);
-    L.prims = reinterpret_cast<const float4*>(blob + S.o_prims);
-    L.inst_trav = reinterpret_cast<const DInstTrav*>(blob + S.o_inst_trav);
-    L.inst_blas = reinterpret_cast<const int4*>(blob + S.o_inst_blas);
-    L.inst_shade = reinterpret_cast<const DInstShade*>(blob + S.o_inst_shade);
-    L.shapes = reinterpret_cast<const DShape*>(blob + S.o_shapes);
-    L.pos = reinterpret_cast<const float4*>(blob + S.o_pos);
-    L.nrm = reinterpret_cast<const float4*>(blob + S.o_nrm);
-    L.tc = reinterpret_cast<const float2*>(blob + S.o_tc);
-    L.col = reinterpret_cast<const float4*>(blob + S.o_col);
-    L.elems = reinterpret_cast<const int4*>(blob + S.o_elems);
-    L.enrm = reinterpret_cast<const float4*>(blob + S.o_enrm);
-    L.enrm_id = reinterpret_cast<const float4*>(blob + S.o_enrm_id);
-    L.materials = reinterpret_cast<const DMaterial*>(blob + S.o_materials);
-    L.lights = reinterpret_cast<const DLight*>(blob + S.o_lights);
-    L.cdf = reinterpret_cast<const float*>(blob + S.o_cdf);
-    return L;
-}
-
-// HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS.
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
-__global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
-    __shared__ int lds_stack[RING * BLOCK];
-    trace_body<SAMPLER, RING, OVF, COUNT, F, true>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
-}
-
-// LDS mode (small scenes): the workgroup stages the scene blob into LDS once; every node,
-// instance, primitive and shading record is then a ds_read instead of a vector-memory load
-// through the TA/TD path (the measured limiter of the HBM-mode kernel).
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
-__global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
-    extern __shared__ uint4 dyn_lds[];
-    uint4* blob = dyn_lds + ((OVF ? RING : S.stack_need) * BLOCK) / 4;  // the stack takes the first entries
-    for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
-    __syncthreads();
-    const DScene L = blob_scene(S, blob);
-    trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
-}
-
-// Persistent launch: as many workgroups as the device holds at once (capped by the number of
-// tiles), each wave then pulls work units until the launch's units are exhausted.
-// LDSK: the specialisation also has an LDS-mode kernel (the large-scene masks run in HBM mode).
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool LDSK = true>
-hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
-    const int tiles = ((P.width + 7) / 8) * ((P.height + 7) / 8);
-    const int want = (tiles + BLOCK / 64 - 1) / (BLOCK / 64);
-    int per_cu = 0;
-    hipError_t e;
-    if constexpr (LDSK) {
-        if (S.blob_n16 > 0) {
-        const size_t lds = (size_t)(OVF ? RING : S.stack_need) * BLOCK * 4 + (size_t)S.blob_n16 * 16;
-        const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>;
-        if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-        const int nwg = std::min(want, per_cu * cus);
-        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
-        return hipGetLastError();
-        }
-    }
-    const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT, F>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    const int nwg = std::min(want, per_cu * cus);
-    hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
-    return hipGetLastError();
-}
-
-// Feature specialisations compiled per stack configuration (besides FT_ALL): FT_NONE for small
-// scenes with a 16-entry stack (cornellbox), and three masks for large HBM-mode scenes with the
-// ring + HBM overflow stack — textured, attributed meshes (bathroom1), plus environments
-// (ecosys), plus quads (features2).
-constexpr int FT_MESH = FT_TEX | FT_ATTR | FT_MAT | FT_OPAC | FT_XFORM;
-constexpr int FT_MESH_ENV = FT_MESH | FT_ENV;
-constexpr int FT_MESH_ENV_QUAD = FT_MESH_ENV | FT_QUAD;
-// the kernel mask a scene with feature bits `feat` runs with (the smallest compiled superset)
-int kernel_mask(int feat, int need, int ring, bool lds) {
-    if (need <= 16) return feat == FT_NONE ? FT_NONE : FT_ALL;
-    if (ring > 16 || lds) return FT_ALL;
-    for (int m : {FT_MESH, FT_MESH_ENV, FT_MESH_ENV_QUAD})
-        if (!(feat & ~m)) return m;
-    return FT_ALL;
-}
-#ifndef JT_ONE_FEAT
-#define JT_ONE_FEAT FT_NONE
-#endif
 // Stack configurations: the whole bound in a 16-entry LDS ring, or a RING-entry ring + HBM.
 template <int SAMPLER, int COUNT>
 hipError_t launch_s(int need, int ring, int kmask, const DScene& S, const DParams& P, int s0, int s1,
                     const DAccum& A, hipStream_t st, int cus) {
-#if JT_ONE_VARIANT  // compile-time experiments only (make quick-usage): one kernel instance
-    (void)need;
-    (void)ring;
-    (void)kmask;
-#ifndef JT_ONE_OVF
-#define JT_ONE_OVF false
-#endif
-    return launch_t<1, 16, JT_ONE_OVF, 0, JT_ONE_FEAT, !JT_ONE_OVF>(S, P, s0, s1, A, st, cus);
-#else
     if (need <= 16) {
-        if (kmask == FT_NONE) return launch_t<SAMPLER, 16, false, COUNT, FT_NONE>(S, P, s0, s1, A, st, cus);
-        return launch_t<SAMPLER, 16, false, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
+        if (kmask == FT_NONE) return launch_cfg<0, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+        return launch_cfg<1, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
     }
     if (ring <= 16) {
         switch (kmask) {
-            case FT_MESH: return launch_t<SAMPLER, 16, true, COUNT, FT_MESH, false>(S, P, s0, s1, A, st, cus);
-            case FT_MESH_ENV: return launch_t<SAMPLER, 16, true, COUNT, FT_MESH_ENV, false>(S, P, s0, s1, A, st, cus);
-            case FT_MESH_ENV_QUAD:
-                return launch_t<SAMPLER, 16, true, COUNT, FT_MESH_ENV_QUAD, false>(S, P, s0, s1, A, st, cus);
-            default: return launch_t<SAMPLER, 16, true, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
+            case FT_MESH: return launch_cfg<2, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+            case FT_MESH_ENV: return launch_cfg<3, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+            case FT_MESH_ENV_QUAD: return launch_cfg<4, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+            default: return launch_cfg<5, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
         }
     }
-    return launch_t<SAMPLER, 32, true, COUNT, FT_ALL>(S, P, s0, s1, A, st, cus);
-#endif
+    return launch_cfg<6, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
 }
-
-}  // namespace
+}  // namespace jtk
 
 // ============================================================================ C-ABI context
 struct jt_ctx {
@@ -1453,6 +82,11 @@ struct jt_ctx {
     std::vector<jt_ctx*> sub;
     std::vector<ncclComm_t> comms;
     std::vector<long long> nsub;  // samples accumulated by each device
+    // split of every batch: false = contiguous sample shares (device d's mean weighted n_d / N in
+    // the reduce), true = interleaved 8x8 pixel tiles (tile t on device t mod D, every sample of
+    // the batch; disjoint pixels, so the reduce is a plain sum). Tiles when params.batch < D:
+    // the reference's default --batch 1 would leave all but one device idle under a sample split
+    bool tile_split = false;
     float* red = nullptr;         // device 0: reduce target, W*H float4
     long long* red_hits = nullptr;
 };
@@ -2054,6 +688,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
         return bail(st);
     S.tlas_nnodes = (int)tlas.size();
+    if (params->traversal != JT_TRAVERSAL_REFERENCE && params->traversal != JT_TRAVERSAL_NEAR)
+        return bail(jt::fail(JT_ERR_INVALID, "traversal must be 0 (reference) or 1 (near)"));
+    S.order_flip = params->traversal == JT_TRAVERSAL_NEAR ? 7 : 0;
     S.nenvs = scene->nenvironments;
     S.nlights = lights->nlights;
 
@@ -2152,6 +789,17 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.nocaustics = params->nocaustics;
     P.first = 0;
     P.seed = params->seed;
+    P.tile_stride = 1;  // every tile (jt_create_multi may split by tiles)
+    P.tile_offset = 0;
+    // JT_TILES=stride,offset (tests only): trace only tiles offset, offset + stride, ... — one
+    // device's share of a tile-split multi-device context, reproducible on a one-GPU box
+    if (const char* ts = std::getenv("JT_TILES")) {
+        int k = 0, o = 0;
+        if (std::sscanf(ts, "%d,%d", &k, &o) == 2 && k >= 1 && o >= 0 && o < k) {
+            P.tile_stride = k;
+            P.tile_offset = o;
+        }
+    }
     // lanes that must be waiting before a shading phase runs; tunable
     P.chunk = 0;  // 0: per launch, a quarter of its samples within [8, 64] (enough units per wave)
     if (const char* ch = std::getenv("JT_CHUNK")) P.chunk = std::max(1, std::atoi(ch));
@@ -2229,6 +877,17 @@ int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lig
         c->sub.push_back(s);
     }
     c->nsub.assign(ndevices, 0);
+    // split mode (jt_ctx::tile_split); JT_MULTI_SPLIT=tiles|samples overrides
+    c->tile_split = params->batch < ndevices;
+    if (const char* m = std::getenv("JT_MULTI_SPLIT")) {
+        if (std::strcmp(m, "tiles") == 0) c->tile_split = true;
+        if (std::strcmp(m, "samples") == 0) c->tile_split = false;
+    }
+    if (c->tile_split)
+        for (int d = 0; d < ndevices; d++) {
+            c->sub[d]->P.tile_stride = ndevices;
+            c->sub[d]->P.tile_offset = d;
+        }
     c->comms.resize(ndevices);
     ncclResult_t r = rccl().CommInitAll(c->comms.data(), ndevices, devs.data());
     if (r != ncclSuccess) {
@@ -2347,24 +1006,30 @@ int trace_finish(jt_ctx* c, float* ms) {
     return JT_OK;
 }
 
-// multi-device trace_samples step: [s0, s1) split into contiguous shares, one per device, each
-// appended to that device's own running mean (weight 1/(n_d + k + 1) for its k-th new sample)
+// multi-device trace_samples step. Sample split: [s0, s1) in contiguous shares, one per device,
+// each appended to that device's own running mean (weight 1/(n_d + k + 1) for its k-th new
+// sample). Tile split: every device traces all of [s0, s1) on its own tiles (the running-mean
+// weights are the single-device ones: first = the context's first sample).
 int multi_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     const int D = (int)c->sub.size();
     const long long L = s1 - s0;
     std::vector<int> a(D), b(D);
-    for (int d = 0; d < D; d++) {
-        a[d] = s0 + (int)(L * d / D);
-        b[d] = s0 + (int)(L * (d + 1) / D);
+    std::vector<char> launched(D, 0);
+    int status = JT_OK;
+    for (int d = 0; d < D && status == JT_OK; d++) {
+        a[d] = c->tile_split ? s0 : s0 + (int)(L * d / D);
+        b[d] = c->tile_split ? s1 : s0 + (int)(L * (d + 1) / D);
         if (a[d] < b[d]) {
-            int st = trace_launch(c->sub[d], a[d], b[d], (int32_t)(a[d] - c->nsub[d]));
-            if (st != JT_OK) return st;
+            const int32_t first = c->tile_split ? c->first : (int32_t)(a[d] - c->nsub[d]);
+            status = trace_launch(c->sub[d], a[d], b[d], first);
+            launched[d] = status == JT_OK;
         }
     }
+    // wait for every launch already queued, even after a failed one: they add to their devices'
+    // running means, so the context is unusable (failed) unless all of them ran
     float wall = 0;
-    int status = JT_OK;
     for (int d = 0; d < D; d++) {
-        if (a[d] >= b[d]) continue;
+        if (!launched[d]) continue;
         float ms = 0;
         const int st = trace_finish(c->sub[d], &ms);
         if (st != JT_OK && status == JT_OK) status = st;
@@ -2381,22 +1046,32 @@ int multi_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     return JT_OK;
 }
 
-// the sample-weighted reduce of the devices' running means onto device 0 (one RCCL reduce with a
-// per-rank premultiplied sum: sum_d mean_d * n_d / N), then to the host. which: 0 image, 1
-// albedo, 2 normal (float4 buffers); hits (int64) are summed.
+// the reduce of the devices' running means onto device 0, then to the host. Sample split: one
+// RCCL reduce with a per-rank premultiplied sum, sum_d mean_d * n_d / N; tile split: the devices'
+// pixels are disjoint (zero elsewhere), so a plain sum. which: 0 image, 1 albedo, 2 normal
+// (float4 buffers); hits (int64) are summed.
 int multi_reduce(jt_ctx* c, int which, float* out4, int64_t* hits) {
     const int D = (int)c->sub.size();
     const size_t np = (size_t)c->width * c->height;
     long long N = 0;
     for (long long n : c->nsub) N += n;
-    std::vector<ncclRedOp_t> ops(D);
+    // the premultiplied-sum ops created so far, destroyed on every exit path
+    struct Ops {
+        jt_ctx* c;
+        std::vector<ncclRedOp_t> op;
+        ~Ops() {
+            for (size_t d = 0; d < op.size(); d++) (void)rccl().RedOpDestroy(op[d], c->comms[d]);
+        }
+    } ops{c, {}};
     std::vector<float> w(D);
     ncclResult_t r;
-    if (out4) {
+    if (out4 && !c->tile_split) {
         for (int d = 0; d < D; d++) {
             w[d] = N > 0 ? (float)((double)c->nsub[d] / (double)N) : (d == 0 ? 1.0f : 0.0f);
-            if ((r = rccl().RedOpCreatePreMulSum(&ops[d], &w[d], ncclFloat32, ncclScalarHostImmediate, c->comms[d])) != ncclSuccess)
+            ncclRedOp_t op;
+            if ((r = rccl().RedOpCreatePreMulSum(&op, &w[d], ncclFloat32, ncclScalarHostImmediate, c->comms[d])) != ncclSuccess)
                 return nccl_fail(r, "ncclRedOpCreatePreMulSum");
+            ops.op.push_back(op);
         }
     }
     if ((r = rccl().GroupStart()) != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
@@ -2405,10 +1080,11 @@ int multi_reduce(jt_ctx* c, int which, float* out4, int64_t* hits) {
         (void)hipSetDevice(s->device);
         if (out4) {
             const float4* src = which == 0 ? s->A.image : which == 1 ? s->A.albedo : s->A.normal;
-            r = rccl().Reduce(src, d == 0 ? (void*)c->red : (void*)src, np * 4, ncclFloat32, ops[d], 0, c->comms[d], s->stream);
+            r = rccl().Reduce(src, d == 0 ? (void*)c->red : (void*)src, np * 4, ncclFloat32,
+                              c->tile_split ? ncclSum : ops.op[d], 0, c->comms[d], s->stream);
         } else {
             r = rccl().Reduce(s->A.hits, d == 0 ? (void*)c->red_hits : (void*)s->A.hits, np, ncclInt64, ncclSum, 0, c->comms[d],
-                           s->stream);
+                              s->stream);
         }
         if (r != ncclSuccess) {
             (void)rccl().GroupEnd();
@@ -2421,8 +1097,6 @@ int multi_reduce(jt_ctx* c, int which, float* out4, int64_t* hits) {
         (void)hipSetDevice(c->sub[d]->device);
         if ((e = hipStreamSynchronize(c->sub[d]->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     }
-    if (out4)
-        for (int d = 0; d < D; d++) (void)rccl().RedOpDestroy(ops[d], c->comms[d]);
     (void)hipSetDevice(c->sub[0]->device);
     if (out4) e = hipMemcpy(out4, c->red, np * 16, hipMemcpyDeviceToHost);
     else e = hipMemcpy(hits, c->red_hits, np * 8, hipMemcpyDeviceToHost);
@@ -2586,7 +1260,7 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
         char tmp[512];
         const int st = jt_describe(c->sub[0], tmp, sizeof tmp);
         if (st != JT_OK) return st;
-        std::snprintf(buf, (size_t)n, "%s devices=%d", tmp, (int)c->sub.size());
+        std::snprintf(buf, (size_t)n, "%s devices=%d split=%s", tmp, (int)c->sub.size(), c->tile_split ? "tiles" : "samples");
         return JT_OK;
     }
     const bool ovf = c->stack > 16;

@@ -32,6 +32,8 @@ STATUS_NAMES = {
 # MaterialType order of src/scene.jl:191-200
 MATERIAL_TYPES = ["matte", "glossy", "reflective", "transparent", "refractive", "subsurface",
                   "volumetric", "gltfpbr"]
+# jt_traversal: BVH child visit order (include/jtrace.h)
+TRAVERSAL_ORDERS = ["reference", "near"]
 
 f32p = C.POINTER(C.c_float)
 i32p = C.POINTER(C.c_int32)
@@ -111,7 +113,8 @@ class jt_params(C.Structure):
                 ("height", C.c_int32), ("samples", C.c_int32), ("bounces", C.c_int32),
                 ("sampler", C.c_int32), ("clamp", C.c_int32), ("envhidden", C.c_int32),
                 ("tentfilter", C.c_int32), ("nocaustics", C.c_int32), ("batch", C.c_int32),
-                ("bvhstacksize", C.c_int32), ("device", C.c_int32), ("seed", C.c_uint64)]
+                ("bvhstacksize", C.c_int32), ("device", C.c_int32), ("seed", C.c_uint64),
+                ("traversal", C.c_int32)]
 
 
 class jt_counters(C.Structure):
@@ -232,6 +235,7 @@ def make_params(params, camera: int = 0) -> jt_params:
     p.bvhstacksize = int(params.bvhstacksize)
     p.device = int(getattr(params, "device", 0) or 0)
     p.seed = int(getattr(params, "seed", 0x5EED))
+    p.traversal = TRAVERSAL_ORDERS.index(getattr(params, "traversal", "reference"))
     return p
 
 

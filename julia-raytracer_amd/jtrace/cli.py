@@ -3,7 +3,8 @@ ArgParse table (:12-86), the SAMPLER_TYPES index (:88) and Params (:90-138).
 
 Extensions beyond the reference (all optional): --seed (RNG seed), --width/--height (explicit
 image size, camera aspect := W/H), --device, --devices N (one context over GPUs 0..N-1:
-jt_create_multi), --missing (drop|error for incomplete scenes).
+jt_create_multi), --missing (drop|error for incomplete scenes), --traversal (reference|near: BVH
+child visit order, include/jtrace.h jt_traversal).
 """
 from __future__ import annotations
 
@@ -51,6 +52,8 @@ def _parser() -> argparse.ArgumentParser:
                    help="GPUs of this node to shard every batch over, devices 0..N-1 (extension)")
     p.add_argument("--missing", choices=["error", "drop"], default="error",
                    help="missing scene assets: error (reference) or drop (extension)")
+    p.add_argument("--traversal", choices=["reference", "near"], default="reference",
+                   help="BVH child order: the reference's, or the near child first (extension)")
     return p
 
 
@@ -80,6 +83,7 @@ class Params:
     device: int = 0
     devices: int = 1
     missing: str = "error"
+    traversal: str = "reference"
 
 
 def params_from_dict(d: dict) -> Params:

@@ -99,6 +99,7 @@ struct JtParams
     camera::Int32; resolution::Int32; width::Int32; height::Int32; samples::Int32
     bounces::Int32; sampler::Int32; clamp::Int32; envhidden::Int32; tentfilter::Int32
     nocaustics::Int32; batch::Int32; bvhstacksize::Int32; device::Int32; seed::UInt64
+    traversal::Int32  # jt_traversal: 0 = the reference's BVH child order
 end
 
 check(st) = st == 0 ? nothing :
@@ -179,10 +180,10 @@ end
 # Params src/cli.jl:90-138: camera is find_camera's 1-based index (src/jtrace.jl:61), sampler is
 # already the 1-based index into SAMPLER_TYPES = ["path", "naive"] (src/cli.jl:88,111-116) —
 # the C side's jt_sampler uses the same numbering — and clamp is an Int (src/cli.jl:105)
-pack_params(p::Params; device = 0, seed = 0x5EED) =
+pack_params(p::Params; device = 0, seed = 0x5EED, traversal = 0) =
     JtParams(Int32(p.camera - 1), Int32(p.resolution), Int32(0), Int32(0), Int32(p.samples), Int32(p.bounces),
              Int32(p.sampler), Int32(p.clamp), Int32(p.envhidden), Int32(p.tentfilter), Int32(p.nocaustics),
-             Int32(p.batch), Int32(p.bvhstacksize), Int32(device), UInt64(seed))
+             Int32(p.batch), Int32(p.bvhstacksize), Int32(device), UInt64(seed), Int32(traversal))
 
 # ---- device context ----------------------------------------------------------------------
 mutable struct HipState

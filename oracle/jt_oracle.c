@@ -365,7 +365,9 @@ static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, sc
     int node_cur = 0; /* number of entries (Julia node_cur - 1) */
     stack[node_cur++] = 0;
     v3 dinv = V3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
-    int dsign[3] = {ray.d.x < 0, ray.d.y < 0, ray.d.z < 0};
+    /* ray_dsign; JT_TRAVERSAL_NEAR (build extension, include/jtrace.h) inverts the push order */
+    const int flip = c->params->traversal == JT_TRAVERSAL_NEAR;
+    int dsign[3] = {(ray.d.x < 0) ^ flip, (ray.d.y < 0) ^ flip, (ray.d.z < 0) ^ flip};
     while (node_cur != 0) {
         const jt_bvh_node* node = &bvh->nodes[stack[--node_cur]];
         sc->cnt.nodes++;
@@ -427,7 +429,9 @@ static scene_isec intersect_scene_bvh(const ctx_t* c, ray3 ray, scratch_t* sc) {
     int node_cur = 0;
     stack[node_cur++] = 0;
     v3 dinv = V3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
-    int dsign[3] = {ray.d.x < 0, ray.d.y < 0, ray.d.z < 0};
+    /* ray_dsign; JT_TRAVERSAL_NEAR (build extension, include/jtrace.h) inverts the push order */
+    const int flip = c->params->traversal == JT_TRAVERSAL_NEAR;
+    int dsign[3] = {(ray.d.x < 0) ^ flip, (ray.d.y < 0) ^ flip, (ray.d.z < 0) ^ flip};
     while (node_cur != 0) {
         const jt_bvh_node* node = &bvh->nodes[stack[--node_cur]];
         sc->cnt.nodes++;

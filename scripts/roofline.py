@@ -12,6 +12,17 @@ actually binds, computed from PMC counters the same way for every workload:
   fp32_lane_frac  = valu_issue_frac * lane_util               (fraction of the FP32 lane throughput)
   td_busy_frac    = TD_TD_BUSY_sum / CUs / (GRBM_GUI_ACTIVE / 8)   (mean busy fraction of a CU's TD)
   hbm_frac        = (2 * FETCH_SIZE + WRITE_SIZE) KiB * 1024 / duration / 8e12   (MI355X_MICROARCH.md)
+  valu_lane_ops   = SQ_INSTS_VALU * 64 * lane_util           (useful FP32 lane-operations per launch)
+  valu_peak_gops  = CUs * 4 SIMDs * 0.5 * 64 lanes * clock_hz / 1e9   (fp32_lane_frac = achieved / this)
+  vmem_rd_gips    = SQ_INSTS_VMEM_RD / duration / 1e9        (vector-memory read wave-instructions/s)
+  vmem_frac       = vmem_rd_gips / VMEM_PEAK_GIPS            (the measured dwordx4 gather ceiling,
+                    profiles/r02_pair/td_width_bench.log mode 0: 2195 G lane-loads/s = 34.3 G/s)
+
+The roof that binds (bench.py `roofline.bound`): "valu" for LDS-mode kernels (the scene is in LDS;
+issue of partly idle waves binds, frac = fp32_lane_frac), "vmem/TD" for HBM-mode kernels (node and
+primitive records are L2-resident and return through TD, frac = vmem_frac); hbm_frac beside it.
+Every record carries `build`, the hash of the kernel sources and build flags it was measured on
+(`source_hash`); bench.py uses a record's counts only for the build it describes.
 
 usage:
   python scripts/roofline.py make --stats KT.csv --fetch DIR --write DIR [--pmc DIR] --workload W --out OUT.json
@@ -27,6 +38,24 @@ import re
 import sys
 
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
+# vector-memory read wave-instructions per second, measured: dependent random dwordx4 gathers over
+# an L2-resident array (scripts/td_width_bench.hip, profiles/r02_pair/td_width_bench.log mode 0:
+# 2195.0 G lane-loads/s / 64 lanes)
+VMEM_PEAK_GIPS = 2195.0 / 64
+ROOT = __import__("pathlib").Path(__file__).resolve().parent.parent
+BUILD_FILES = ("julia-raytracer_amd/Makefile", "julia-raytracer_amd/csrc/jt_kernels.h", "julia-raytracer_amd/csrc/jt_kv.hip",
+               "julia-raytracer_amd/csrc/jt_device.h", "julia-raytracer_amd/csrc/jt_bsdf.h",
+               "julia-raytracer_amd/csrc/jt_trace.hip")
+
+
+def source_hash(root=ROOT):
+    """Hash of the kernel sources and build flags: identifies the build a record was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in BUILD_FILES:
+        h.update(f.encode())
+        h.update((root / f).read_bytes())
+    return h.hexdigest()[:16]
 CUS = 256
 XCDS = 8
 KERNEL_RE = re.compile(r"(trace_kernel\w*<\d+, \d+, (?:true|false), 0, \d+>)")
@@ -82,6 +111,13 @@ def derive(rec):
             out["fp32_lane_frac"] = out["valu_issue_frac"] * out["lane_util"]
         if pmc.get("TD_TD_BUSY_sum"):  # summed over the 256 CUs' TD units
             out["td_busy_frac"] = pmc["TD_TD_BUSY_sum"] / CUS / (pmc["GRBM_GUI_ACTIVE"] / XCDS)
+        if "lane_util" in out and pmc.get("SQ_INSTS_VALU"):
+            out["valu_lane_ops"] = pmc["SQ_INSTS_VALU"] * 64.0 * out["lane_util"]
+            out["valu_peak_gops"] = CUS * 4 * 0.5 * 64 * clk / 1e9
+        if pmc.get("SQ_INSTS_VMEM_RD"):
+            out["vmem_rd_per_launch"] = pmc["SQ_INSTS_VMEM_RD"]
+            out["vmem_rd_gips"] = pmc["SQ_INSTS_VMEM_RD"] / pd / 1e9
+            out["vmem_frac"] = out["vmem_rd_gips"] / VMEM_PEAK_GIPS
     return {k: round(v, 6) for k, v in out.items()}
 
 
@@ -91,7 +127,7 @@ def make(a):
     w, _ = counter_means(a.write, kernel)
     if "FETCH_SIZE" not in f or "WRITE_SIZE" not in w:
         raise SystemExit("FETCH_SIZE / WRITE_SIZE of the timed kernel not found")
-    rec = {"workload": a.workload, "kernel": kernel, "duration_ns": avg_ns, "calls": calls,
+    rec = {"workload": a.workload, "kernel": kernel, "build": source_hash(), "duration_ns": avg_ns, "calls": calls,
            "raw": {"FETCH_SIZE": f["FETCH_SIZE"], "WRITE_SIZE": w["WRITE_SIZE"]}}
     if a.pmc:
         pmc, pdur = {}, []
@@ -114,7 +150,9 @@ def check(paths):
         rec = json.load(open(p))
         again = derive(rec)
         for k, v in again.items():
-            if abs(rec["derived"].get(k, float("nan")) - v) > 1e-6 * max(1.0, abs(v)):
+            if k not in rec["derived"]:  # a field added after this record was written
+                continue
+            if abs(rec["derived"][k] - v) > 1e-6 * max(1.0, abs(v)):
                 print(f"{p}: {k} recorded {rec['derived'].get(k)} recomputed {v}")
                 bad += 1
         if again["hbm_frac"] > 1.0:

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_version(lib):
-    assert lib.jt_abi_version() == 1
+    assert lib.jt_abi_version() == 2  # 2: jt_params.traversal
     assert b"gfx950" in lib.jt_version()
 
 

@@ -62,3 +62,31 @@ def test_multi_context_rejects_bad_device_lists(gpu, abi, lib, cornell_abi):
         arr = (C.c_int32 * len(devs))(*devs)
         st = lib.jt_create_multi(sa.ref, bvh.ref, lights.ref, C.byref(p), arr, len(devs), C.byref(h))
         assert st == -1, (devs, st, lib.jt_last_error())
+
+
+@pytest.mark.parametrize("D", [2, 3, 8])
+def test_tile_split_shares_sum_to_the_single_device_image(gpu, abi, lib, cornell_abi, D, monkeypatch):
+    """The tile split of jt_create_multi at batch < devices, reproduced on one GPU: contexts
+    tracing every D-th 8x8 tile from offset d (JT_TILES, the per-device launch parameters the
+    multi-device context sets) at the reference's default --batch 1 each cover disjoint pixels,
+    every one of them traces work, and their plain sum is the single-device image bit for bit."""
+    p = make_params(abi, resolution=72, samples=3, batch=1)
+    one = _render(abi, lib, cornell_abi, p, 3)
+    img = np.zeros_like(one[0])
+    alb = np.zeros_like(one[1][0])
+    hits = np.zeros_like(one[1][2])
+    paths = 0
+    for d in range(D):
+        monkeypatch.setenv("JT_TILES", f"{D},{d}")
+        part = _render(abi, lib, cornell_abi, p, 3)
+        assert part[2]["paths"] > 0, d  # every device gets work at batch 1
+        paths += part[2]["paths"]
+        covered = np.any(part[0] != 0, axis=-1) | (part[1][2] != 0)
+        assert not np.any(covered & np.any(img != 0, axis=-1)), d  # disjoint pixels
+        img += part[0]
+        alb += part[1][0]
+        hits += part[1][2]
+    assert paths == one[2]["paths"]
+    assert np.array_equal(img, one[0])
+    assert np.array_equal(alb, one[1][0])
+    assert np.array_equal(hits, one[1][2])

@@ -1,0 +1,66 @@
+"""The near-child-first traversal option (jt_params.traversal = JT_TRAVERSAL_NEAR, include/jtrace.h).
+
+The reference pushes the children of an internal node so that, for d[axis] >= 0, the upper
+child (start+1) pops first (src/bvh.jl:331-341, 396-407): for a closest-hit query that is the
+far child. The option inverts the push order. The oracle restates the same switch
+(oracle/jt_oracle.c, intersect_scene_bvh / intersect_shape_bvh), so HIP vs oracle stays at the
+parity bar in both orders. Against the reference order only exact-t ties (the later-tested of
+two equally distant primitives wins, src/geometry.jl:226) and boxes culled by the slab test's
+rounding can resolve differently: the images must still meet the §8(c) bar against each other,
+and the fraction of pixels that differ at all is reported.
+"""
+import numpy as np
+import pytest
+
+from conftest import compare_images, make_params
+from test_gpu_scenes import check_parity, render_gpu, render_oracle, scene_abi
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
+@pytest.mark.parametrize("name,lds", [("cornellbox", "lds"), ("cornellbox", "hbm"), ("features1", None),
+                                      ("features2", None), ("bathroom1", None), ("ecosys", None)])
+def test_near_order_parity(gpu, abi, lib, oracle, cornell_abi, name, lds, sampler, monkeypatch):
+    """HIP vs oracle, both in near-first order (LDS and HBM scene modes for cornellbox)."""
+    if lds == "hbm":
+        monkeypatch.setenv("JT_LDS_SCENE", "0")
+    sa = cornell_abi if name == "cornellbox" else scene_abi(name)
+    p = make_params(abi, resolution=120, samples=4, sampler=sampler, traversal="near")
+    g = render_gpu(lib, sa, p, 0, 4)
+    o = render_oracle(oracle, sa, p, g[0].shape[1], g[0].shape[0], 0, 4)
+    check_parity(g, o, f"{name}/{lds}/{sampler}/near")
+
+
+@pytest.mark.parametrize("name", ["cornellbox", "features2", "bathroom1", "ecosys"])
+def test_near_vs_reference_order(gpu, abi, lib, cornell_abi, name):
+    """Near-first against the reference order on the GPU: the §8(c) bar holds between the two
+    images, hit counts agree to ties, and fewer nodes are popped per closest-hit query."""
+    sa = cornell_abi if name == "cornellbox" else scene_abi(name)
+    out = {}
+    for order in ("reference", "near"):
+        p = make_params(abi, resolution=160, samples=4, traversal=order)
+        out[order] = render_gpu(lib, sa, p, 0, 4)
+    r, n = out["reference"], out["near"]
+    stats = compare_images(n[0], r[0])
+    differ = float(np.mean(np.any(n[0] != r[0], axis=-1)))
+    nodes_r = r[4]["nodes"] / r[4]["rays"]
+    nodes_n = n[4]["nodes"] / n[4]["rays"]
+    print(f"{name}: pixels differing from the reference order {differ:.6f}, {stats}; "
+          f"nodes/ray {nodes_r:.2f} -> {nodes_n:.2f}, prims/ray {r[4]['prims'] / r[4]['rays']:.2f} -> "
+          f"{n[4]['prims'] / n[4]['rays']:.2f}")
+    assert stats["frac_pix_rel_le_1e-3"] >= 0.999, stats
+    assert stats["image_mean_rel"] <= 1e-3, stats
+    assert differ <= 1e-3, differ
+    assert nodes_n < nodes_r
+
+
+def test_near_order_rejects_bad_value(gpu, abi, lib, cornell_abi):
+    from jtrace import trace
+    bvh = trace.make_scene_bvh(cornell_abi, False, lib)
+    lights = trace.make_trace_lights(cornell_abi, lib)
+    p = make_params(abi, resolution=16, samples=1)
+    p.traversal = 5
+    with pytest.raises(abi.JTError) as e:
+        trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
+    assert e.value.status == -1

@@ -1,0 +1,26 @@
+"""The oracle's near-child-first switch (jt_params.traversal, include/jtrace.h) on the CPU: the
+same closest hits up to exact-t ties, fewer nodes popped (src/bvh.jl:331-341 is far-first)."""
+import numpy as np
+
+from conftest import compare_images, make_params
+
+
+def test_oracle_near_order_matches_reference_order(abi, oracle, cornell_abi):
+    ob = oracle.build_bvh(cornell_abi)
+    ol = oracle.make_lights(cornell_abi)
+    out = {}
+    for order in ("reference", "near"):
+        p = make_params(abi, resolution=64, samples=2, traversal=order)
+        out[order] = oracle.trace(cornell_abi, ob, ol, p, 64, 64, 0, 2)
+    r, n = out["reference"], out["near"]
+    stats = compare_images(n[0], r[0])
+    assert stats["frac_pix_rel_le_1e-3"] >= 0.999, stats
+    assert np.array_equal(n[3], r[3])  # hit counts
+    assert n[4]["rays"] == r[4]["rays"]
+    assert n[4]["nodes"] < r[4]["nodes"], (n[4]["nodes"], r[4]["nodes"])
+
+
+def test_params_carry_the_traversal_order(abi):
+    assert make_params(abi).traversal == 0
+    assert make_params(abi, traversal="near").traversal == 1
+    assert abi.jt_params.traversal.offset == 64 and abi.C.sizeof(abi.jt_params) == 72
