@@ -275,8 +275,8 @@ struct Hit {
     float u, v, t;
     bool hit;
 };
-struct Counters {
-    unsigned rays, light_queries, nodes, instances, prims, shades, paths;
+struct Counters {  // diagnostic traversal counts (COUNT=1); paths / rays / light queries are per wave
+    unsigned nodes, instances, prims, shades;
 };
 
 // A resumable BVH query per lane, for intersect_scene_bvh (root = TLAS node 0) and
@@ -629,7 +629,7 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
         st.li += 1;
         if (st.li >= S.nlights) {
             st.o = st.lq;  // the next bounce's ray starts at the shading position
-            const float pdf = st.pdf * sample_uniform_pdf(S.nlights);
+            const float pdf = st.pdf * S.light_pick_pdf;  // sample_uniform_pdf(nlights), host-computed
             st.weight = st.weight / (0.5f * st.pb + 0.5f * pdf);  // (weight .* f) / (...)
             return after_weight(P, st);
         }
@@ -990,13 +990,21 @@ template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
                                            int* stack) {
     const int lane = threadIdx.x & 63;
-    Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    // WC: paths, scene rays and light queries are counted per wave (ballots at wave-uniform
-    // points, scalar registers), not per lane: three fewer VGPRs live across the traversal loop.
-    // The mesh kernels gain (bathroom1 +3 %, features2 +1 %); the FT_NONE kernel, whose light-hit
-    // steps run the ballots every few iterations, loses 1.5 % and keeps per-lane counters.
+    Counters cnt{0, 0, 0, 0};
+    // Paths, scene rays and light queries are counted per wave, never in per-lane registers
+    // (three VGPRs live across the traversal loop, spilled and written back every shading
+    // phase: 14 GB of scratch write-back per cornellbox launch).
+    // WC (mesh kernels): ballots at wave-uniform points, summed in scalar registers (bathroom1
+    // +3 %, features2 +1 % over per-lane counters). The FT_NONE kernel, whose light-hit steps run
+    // every few iterations, adds to three per-wave LDS words instead (ds_add, no ballot).
     constexpr bool WC = F != FT_NONE;
     unsigned w_paths = 0, w_rays = 0, w_lq = 0;
+    __shared__ unsigned wave_cnt[WC ? 1 : (BLOCK / 64) * 4];
+    unsigned* const wcnt = wave_cnt + (WC ? 0 : (threadIdx.x >> 6) * 4);
+    if (!WC && lane < 3) wcnt[lane] = 0u;
+    auto lds_count = [&](int k, bool c) {
+        if (c) __hip_atomic_fetch_add(wcnt + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
     constexpr bool LL = lane_lds(F);
     __shared__ float acc_lds[acc_slots(F) * BLOCK];
     float* acc = acc_lds + threadIdx.x;
@@ -1066,7 +1074,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         query_begin(S, T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
     }
     if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(alive));
-    else cnt.rays += alive ? 1 : 0;
+    else lds_count(1, alive);
     for (;;) {
 #if JT_STAMPS
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -1098,11 +1106,11 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                             st.phase = PH_FINISH;
                         } else if (st.phase == PH_LIGHT) {
                             if (WC) c_lq = true;
-                            else cnt.light_queries++;
+                            else lds_count(2, true);
                             query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
                         } else {
                             if (WC) c_ray = true;
-                            else cnt.rays++;
+                            else lds_count(1, true);
                             query_begin(S, T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
                         }
                     }
@@ -1172,7 +1180,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (done) {
                 // trace_sample epilogue (src/trace.jl:625-648)
                 if (WC) c_path = true;
-                else cnt.paths++;
+                else lds_count(0, true);
                 v3 radiance = st.radiance;
                 if (!all_finite(radiance)) radiance = V3(0, 0, 0);
                 const float mr = max3(radiance);
@@ -1220,11 +1228,11 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (alive) {
                 if (SAMPLER == 1 && st.phase == PH_LIGHT) {
                     if (WC) c_lq = true;
-                    else cnt.light_queries++;
+                    else lds_count(2, true);
                     query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
                 } else {
                     if (WC) c_ray = true;
-                    else cnt.rays++;
+                    else lds_count(1, true);
                     query_begin(S, T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
                 }
                 // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
@@ -1282,13 +1290,12 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         atomicAdd(dbg + 15, dead_lanes);
     }
 #endif
-    // one atomic per counter per wave
+    // one atomic per counter per wave (the wave's own LDS adds precede this read in program order)
     const unsigned wv[3] = {w_paths, w_rays, w_lq};
-    unsigned v[7] = {cnt.paths, cnt.rays, cnt.light_queries, cnt.nodes, cnt.instances, cnt.prims,
-                     COUNT ? cnt.shades : 0u};
+    unsigned v[7] = {0u, 0u, 0u, cnt.nodes, cnt.instances, cnt.prims, COUNT ? cnt.shades : 0u};
 #pragma unroll
     for (int k = 0; k < 7; k++) {
-        unsigned s = (WC && k < 3) ? wv[k] : wave_sum(v[k]);
+        unsigned s = k < 3 ? (WC ? wv[k] : wcnt[k]) : wave_sum(v[k]);
         if (lane == 0 && s) atomicAdd(&A.counters[k], (unsigned long long)s);
     }
 }

@@ -693,6 +693,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     S.order_flip = params->traversal == JT_TRAVERSAL_NEAR ? 7 : 0;
     S.nenvs = scene->nenvironments;
     S.nlights = lights->nlights;
+    S.light_pick_pdf = lights->nlights > 0 ? (float)(1.0 / (double)lights->nlights) : 0.0f;
 
     // ------------------------------------------------------------- small-scene LDS blob
     {
