@@ -75,14 +75,14 @@ def roofline_record(workload: str, kernel: str, build: str):
     return None, None
 
 
-def cpu_baseline(scene_abi, params, width, height, nthreads, spp=2):
+def cpu_baseline(scene_abi, params, width, height, nthreads, spp=2, high_quality=False):
     """Oracle (C restatement, oracle/jt_oracle.c) on host cores: bounded sample of the same
     workload — all pixels, samples [0, spp)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     from jtrace import abi
     from oracle import Oracle  # the checker, timed as the CPU baseline only
     orc = Oracle(abi)
-    ob = orc.build_bvh(scene_abi)
+    ob = orc.build_bvh(scene_abi, high_quality)
     ol = orc.make_lights(scene_abi)
     t0 = time.perf_counter()
     _, _, _, _, cnt = orc.trace(scene_abi, ob, ol, params, width, height, 0, spp, nthreads=nthreads)
@@ -103,8 +103,13 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--sampler", default="path")
     ap.add_argument("--scene", default=str(ROOT / "assets" / "scenes" / "cornellbox" / "cornellbox.json"))
-    ap.add_argument("--traversal", choices=["reference", "near"], default="reference",
-                    help="BVH child order (include/jtrace.h jt_traversal); the headline uses the reference's")
+    ap.add_argument("--traversal", choices=["reference", "near"], default="near",
+                    help="BVH child order (include/jtrace.h jt_traversal): near child first (the default, the "
+                         "product's order) or the reference's far-first order (src/bvh.jl:331-341)")
+    ap.add_argument("--no-reference-order", action="store_true",
+                    help="skip the reference-order comparison line (rank 0, N=1, --traversal near)")
+    ap.add_argument("--highqualitybvh", action="store_true",
+                    help="the reference's SAH build (--highqualitybvh, src/bvh.jl:218-274) instead of split_middle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-spp", type=int, default=128)
@@ -142,7 +147,7 @@ def main():
     params = Params(scene=args.scene, samples=args.spp, sampler=2 if args.sampler == "naive" else 1,
                     width=args.width, height=args.height, device=dev, batch=args.spp, traversal=args.traversal)
     jp = abi.make_params(params, 0)
-    bvh = trace.make_scene_bvh(sa, False, lib)
+    bvh = trace.make_scene_bvh(sa, args.highqualitybvh, lib)
     t_bvh = time.perf_counter()
     lights = trace.make_trace_lights(sa, lib)
     t_lights = time.perf_counter()
@@ -212,12 +217,48 @@ def main():
     else:
         total_rays = float(rays)
 
+    # Reference-order leg (rank 0, N=1): the same workload with the reference's far-child-first
+    # order (src/bvh.jl:331-341, SURVEY Appendix B item 9: performance only), timed the same way,
+    # and the fraction of pixels whose final running mean differs from the near-first image (only
+    # exact-t ties can resolve differently)
+    ref_order = None
+    if rank == 0 and world == 1 and args.traversal != "reference" and not args.no_reference_order:
+        img_near = state.get_image()
+        rp = abi.make_params(Params(scene=args.scene, samples=args.spp, sampler=2 if args.sampler == "naive" else 1,
+                                    width=args.width, height=args.height, device=dev, batch=args.spp,
+                                    traversal="reference"), 0)
+        rst = trace.make_trace_state(sa, bvh, lights, rp, lib)
+        rst.set_counters(1)
+        rst.trace_range(s0, s1)
+        rfull = rst.counters()
+        rst.set_counters(0)
+        for _ in range(args.warmup):
+            rst.reset()
+            rst.trace_range(s0, s1)
+        torch.cuda.synchronize()
+        r0 = time.perf_counter()
+        rrays = 0
+        for _ in range(args.steps):
+            rst.reset()
+            rst.trace_range(s0, s1)
+            rrays += rst.counters()["rays"]
+        torch.cuda.synchronize()
+        relapsed = time.perf_counter() - r0
+        img_ref = rst.get_image()
+        rst.close()
+        ref_order = {"traversal": "reference", "value": round(rrays / relapsed / 1e6, 2),
+                     "ms_per_step": round(relapsed / args.steps * 1e3, 3),
+                     "speedup_of_near": round((total_rays / elapsed) / (rrays / relapsed), 4),
+                     "pixels_differing_from_near": float(np.mean(np.any(img_ref != img_near, axis=-1))),
+                     "per_ray": {k: round(rfull[k] / max(1, rfull["rays"]), 3)
+                                 for k in ("nodes", "instances", "prims", "shades", "light_queries")}}
+
     # CPU baseline leg (rank 0, N=1): the oracle on host cores over samples [0, cpu_spp) of this
     # workload; the GPU then re-traces exactly those samples so the two ray counts — hence the
     # two cameras and framings — are checked to agree (a libm ulp may flip a rare path: <= 0.1 %)
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(sa, jp, W, H, args.cpu_threads, args.cpu_spp)
+        cpu = cpu_baseline(sa, jp, W, H, args.cpu_threads, args.cpu_spp, args.highqualitybvh)
         state.reset()
         state.trace_range(0, args.cpu_spp)
         g = state.counters()
@@ -238,7 +279,8 @@ def main():
         logical = algorithmic_bytes(per_launch, shade_record_bytes(scene),
                                     any(len(s.quads) for s in scene.shapes))
         workload = f"{name} {args.sampler} {W}x{H} {s1 - s0} samples/launch" + \
-            ("" if args.traversal == "reference" else f" traversal={args.traversal}")
+            ("" if args.traversal == "reference" else f" traversal={args.traversal}") + \
+            (" bvh=sah" if args.highqualitybvh else "")
         sys.path.insert(0, str(ROOT / "scripts"))
         from roofline import VMEM_PEAK_GIPS, source_hash
         build = source_hash()
@@ -287,8 +329,7 @@ def main():
                 "per_ray": {k: round(per_launch[k] / max(1.0, per_launch["rays"]), 3)
                             for k in ("nodes", "instances", "prims", "shades", "light_queries")}})
         line = {
-            "metric": metric_name(name, args.sampler, W, H, S) + ("" if args.traversal == "reference" else
-                                                                   f" (traversal={args.traversal})"),
+            "metric": metric_name(name, args.sampler, W, H, S) + (" (--highqualitybvh)" if args.highqualitybvh else ""),
             "value": round(value, 2), "unit": "Mrays/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
@@ -296,13 +337,14 @@ def main():
                     + (f"; {'; '.join(scene.notes)}" if scene.notes else ""),
             "config": {"workload": f"{name} {args.sampler} {W}x{H}x{S}spp", "scene": name,
                        "sampler": args.sampler, "width": W, "height": H, "spp": S, "bounces": 8,
-                       "traversal": args.traversal,
+                       "traversal": args.traversal, "bvh": "sah" if args.highqualitybvh else "middle",
                        "parallelism": f"sample-range shards x{world} + RCCL reduce"},
             "render_s": round(ms_per_step / 1e3, 4),
             "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 2),
             "mlight_queries_per_s": round(agg["light_queries"] * world / elapsed / 1e6, 2),
             "time_to_first_pixel_s": ttfp,
             "roofline": roof,
+            "reference_order": ref_order,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

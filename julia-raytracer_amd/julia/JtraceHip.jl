@@ -180,7 +180,10 @@ end
 # Params src/cli.jl:90-138: camera is find_camera's 1-based index (src/jtrace.jl:61), sampler is
 # already the 1-based index into SAMPLER_TYPES = ["path", "naive"] (src/cli.jl:88,111-116) —
 # the C side's jt_sampler uses the same numbering — and clamp is an Int (src/cli.jl:105)
-pack_params(p::Params; device = 0, seed = 0x5EED, traversal = 0) =
+# traversal: 1 = near child first (jt_traversal, the product default: the reference's far-first
+# order, src/bvh.jl:331-341, is performance-only; only exact-t ties resolve differently), 0 = the
+# reference's order
+pack_params(p::Params; device = 0, seed = 0x5EED, traversal = 1) =
     JtParams(Int32(p.camera - 1), Int32(p.resolution), Int32(0), Int32(0), Int32(p.samples), Int32(p.bounces),
              Int32(p.sampler), Int32(p.clamp), Int32(p.envhidden), Int32(p.tentfilter), Int32(p.nocaustics),
              Int32(p.batch), Int32(p.bvhstacksize), Int32(device), UInt64(seed), Int32(traversal))

@@ -7,7 +7,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 out=$1; workload=$2; shift 2
 mkdir -p $out
-B="bench.py --steps ${MEASURE_STEPS:-2} --warmup ${MEASURE_WARMUP:-1} --no-cpu-baseline $*"
+B="bench.py --steps ${MEASURE_STEPS:-2} --warmup ${MEASURE_WARMUP:-1} --no-cpu-baseline --no-reference-order $*"
 scripts/gpu_step.sh 300 $out/kt.log rocprofv3 --kernel-trace --stats --output-format csv -d $out/kt -o kt -- python3 $B || exit 1
 scripts/gpu_step.sh 300 $out/fetch.log timeout -s KILL 280 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o fetch -- python3 $B || exit 1
 scripts/gpu_step.sh 300 $out/write.log timeout -s KILL 280 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o write -- python3 $B || exit 1

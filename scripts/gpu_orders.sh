@@ -23,3 +23,7 @@ for l in open('$f'):
     if l.startswith('{'):
         d=json.loads(l); r=d['roofline']; print('$f'.split('/')[-1], d['value'], 'ms/step', d['ms_per_step'], 'per_ray', r['per_ray'])
 "; done
+# optional library A/B on the same box: ORDERS_AB="<lib> ..." (lib .so names under julia-raytracer_amd/build)
+if [ -n "$ORDERS_AB" ]; then
+  AB_SCENES="cb f2 b1" bash scripts/gpu_lib_ab.sh $1/ab base $ORDERS_AB || exit 1
+fi

@@ -10,5 +10,5 @@ if [ "$2" != "skip-tests" ]; then
   scripts/gpu_step.sh 900 $O/pytest.log python -u -m pytest tests -x -v -m gpu -rf --timeout 300 --timeout-method thread || exit 1
 fi
 scripts/gpu_step.sh 400 $O/bench.log python bench.py || exit 1
-bash scripts/gpu_measure.sh $O/cb "cornellbox path 1280x720 256 samples/launch" || exit 1
+bash scripts/gpu_measure.sh $O/cb "cornellbox path 1280x720 256 samples/launch traversal=near" || exit 1
 nproc > $O/host.txt; lscpu | grep -E "Model name|Socket|Core|Thread" >> $O/host.txt
