@@ -589,14 +589,26 @@ __device__ __forceinline__ float env_light_pdf(const DScene& S, const DLight l, 
 enum : int { PH_SCENE = 0, PH_LIGHT = 1, PH_FINISH = 2 };  // PH_FINISH: path done, sample not yet accumulated
 enum : int { F_HIT = 1, F_VOLUME = 2 };
 
+// The path's small counters share one register (they are read only in the shading code, and as
+// separate registers they were spilled and written back every shading phase):
+//   bits 0-14 bounce (jt_create rejects bounces > 32766), 15-22 opbounce (<= 129),
+//   23-24 flags (F_HIT, F_VOLUME), 25-31 lcount (the light-query chain, < 100).
+constexpr unsigned CTL_BOUNCE = 0x7fffu, CTL_OPB = 15, CTL_FLAGS = 23, CTL_LC = 25;
 struct Path {
     v3 o, d;                    // pending ray (during PH_LIGHT the light query's: origin / incoming)
     v3 radiance, weight;  // during PH_LIGHT weight already holds weight .* f (src/trace.jl:386)
     Rng rng;
-    int bounce, opbounce, flags, phase;
+    unsigned ctl;  // bounce | opbounce | flags | lcount (CTL_*)
+    int phase;
     float max_roughness;
     // sample_lights_pdf in flight (src/trace.jl:1010-1084)
-    int li, lcount;
+    int li;
+    __device__ __forceinline__ int bounce() const { return (int)(ctl & CTL_BOUNCE); }
+    __device__ __forceinline__ int opbounce() const { return (int)((ctl >> CTL_OPB) & 0xffu); }
+    __device__ __forceinline__ bool flag(int f) const { return (ctl >> CTL_FLAGS) & (unsigned)f; }
+    __device__ __forceinline__ void set_flag(int f) { ctl |= (unsigned)f << CTL_FLAGS; }
+    __device__ __forceinline__ void clear_flag(int f) { ctl &= ~((unsigned)f << CTL_FLAGS); }
+    __device__ __forceinline__ int lcount() const { return (int)(ctl >> CTL_LC); }
     v3 lq;       // during PH_LIGHT: the shading position (st.o holds the light query's origin,
                  // next_position of src/trace.jl:1039, so every query's ray is (st.o, st.d))
     float pb;    // sample_bsdfcos_pdf / sample_scattering_pdf
@@ -606,15 +618,22 @@ struct Path {
 
 // while bounce < params.bounces: bounce += 1 (src/trace.jl:295-297, 487-489)
 __device__ __forceinline__ bool next_bounce(const DParams& P, Path& st) {
-    if (st.bounce >= P.bounces) return true;
-    st.bounce += 1;
+    if (st.bounce() >= P.bounces) return true;
+    st.ctl += 1u;  // bounce += 1
+    st.phase = PH_SCENE;
+    return false;
+}
+// the opacity retry (src/trace.jl:334-339): bounce -= 1, then the loop's bounce += 1, i.e. the
+// loop condition tested with bounce - 1 and bounce unchanged
+__device__ __forceinline__ bool next_bounce_retry(const DParams& P, Path& st) {
+    if (st.bounce() - 1 >= P.bounces) return true;
     st.phase = PH_SCENE;
     return false;
 }
 // end of a bounce: weight checks and Russian roulette (src/trace.jl:455-465, 557-567)
 __device__ __forceinline__ bool after_weight(const DParams& P, Path& st) {
     if (is_zero(st.weight) || !all_finite(st.weight)) return true;
-    if (st.bounce > 3) {
+    if (st.bounce() > 3) {
         float rr_prob = jl_min(0.99f, max3(st.weight));
         if (rand1f(st.rng) >= rr_prob) return true;
         st.weight = st.weight * (1 / rr_prob);
@@ -636,7 +655,7 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
         const DLight l = S.lights[st.li];
         if (l.instance >= 0) {
             st.lpdf = 0.0f;
-            st.lcount = 0;
+            st.ctl &= (1u << CTL_LC) - 1u;  // lcount = 0
             st.o = st.lq;  // the first query starts at the shading position
             st.phase = PH_LIGHT;
             return false;
@@ -662,7 +681,8 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
         v3 dd = lposition - st.lq;
         st.lpdf += dot(dd, dd) / (__builtin_fabsf(dot(lnormal, st.d)) * area);
         st.o = lposition + st.d * 0.001f;
-        if (++st.lcount < 100) return false;
+        st.ctl += 1u << CTL_LC;  // lcount += 1 (< 100: fits its 7 bits)
+        if (st.lcount() < 100) return false;
     }
     st.pdf += st.lpdf;
     return light_advance<F>(S, P, st);
@@ -722,11 +742,11 @@ template <int F, class AovT>
 __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const AovT& aov,
                                          unsigned& shades) {
     if (!isec.hit) {
-        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
+        if (st.bounce() > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
         return true;
     }
     bool in_volume = false;
-    if ((F & FT_VOL) && (st.flags & F_VOLUME)) {  // :307-326 (volumes need a volume material)
+    if ((F & FT_VOL) && st.flag(F_VOLUME)) {  // :307-326 (volumes need a volume material)
         float rl = rand1f(st.rng), rd = rand1f(st.rng);
         float distance = sample_transmittance(st.vol.density, isec.t, rl, rd);
         v3 tr = eval_transmittance(st.vol.density, distance);
@@ -745,14 +765,13 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
             sh.mat.roughness = st.max_roughness;
         }
         if ((F & FT_OPAC) && sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
-            if (st.opbounce > 128) return true;
-            st.opbounce += 1;
+            if (st.opbounce() > 128) return true;
+            st.ctl += 1u << CTL_OPB;  // opbounce += 1 (<= 129)
             st.o = sh.position + st.d * 0.01f;
-            st.bounce -= 1;
-            return next_bounce(P, st);
+            return next_bounce_retry(P, st);  // bounce -= 1, then the loop's bounce += 1
         }
-        if (st.bounce == 0) {
-            st.flags |= F_HIT;
+        if (st.bounce() == 0) {
+            st.set_flag(F_HIT);
             aov_update<F>(aov, sh.mat.color, sh.normal);
         }
         st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
@@ -782,13 +801,13 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
         const int mtype = sh.mat.type;
         if ((F & FT_VOL) && (mtype == M_REFRACTIVE || mtype == M_VOLUMETRIC || mtype == M_SUBSURFACE) &&
             dot(sh.normal, outgoing) * dot(sh.normal, incoming) < 0) {
-            if (!(st.flags & F_VOLUME)) {
-                st.flags |= F_VOLUME;  // eval_material again: only the volume fields are kept
+            if (!st.flag(F_VOLUME)) {
+                st.set_flag(F_VOLUME);  // eval_material again: only the volume fields are kept
                 st.vol.density = sh.mat.density;
                 st.vol.scattering = sh.mat.scattering;
                 st.vol.scanisotropy = sh.mat.scanisotropy;
             } else {
-                st.flags &= ~F_VOLUME;
+                st.clear_flag(F_VOLUME);
             }
         }
         st.o = sh.position;
@@ -821,7 +840,7 @@ template <int F, class AovT>
 __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const AovT& aov,
                                           unsigned& shades) {
     if (!isec.hit) {
-        if (st.bounce > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
+        if (st.bounce() > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
         return true;
     }
     v3 outgoing = -st.d;
@@ -829,14 +848,13 @@ __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Pat
     eval_shading<F>(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
     shades++;
     if ((F & FT_OPAC) && sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
-        if (st.opbounce > 128) return true;
-        st.opbounce += 1;
+        if (st.opbounce() > 128) return true;
+        st.ctl += 1u << CTL_OPB;  // opbounce += 1 (<= 129)
         st.o = sh.position + st.d * 0.01f;
-        st.bounce -= 1;
-        return next_bounce(P, st);
+        return next_bounce_retry(P, st);  // bounce -= 1, then the loop's bounce += 1
     }
-    if (st.bounce == 0) {
-        st.flags |= F_HIT;
+    if (st.bounce() == 0) {
+        st.set_flag(F_HIT);
         aov_update<F>(aov, sh.mat.color, sh.normal);
     }
     st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
@@ -903,9 +921,7 @@ __device__ __forceinline__ void start_path(const DParams& P, int i, int j, int p
     st.radiance = V3(0, 0, 0);
     st.weight = V3(1, 1, 1);
     st.max_roughness = 0.0f;
-    st.bounce = 0;  // the first loop iteration: bounce = -1 + 1 (bounces >= 0 always enters)
-    st.opbounce = 0;
-    st.flags = 0;
+    st.ctl = 0u;  // bounce 0 (the first loop iteration: -1 + 1; bounces >= 0 always enters), no flags
     st.phase = PH_SCENE;
 }
 
@@ -1187,7 +1203,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
                 const float w = aov.w<F>();
                 const float omw = 1 - w;
-                const bool hit = st.flags & F_HIT;
+                const bool hit = st.flag(F_HIT);
                 const bool env = !hit && !P.envhidden && S.nenvs != 0;
                 const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
                 // no bounce-0 surface was accepted: st.d is still the camera ray direction

@@ -300,6 +300,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         return jt::fail(JT_ERR_INVALID, "sampler must be 1 (path) or 2 (naive)");
     if (params->samples < 0 || params->bounces < 0 || params->batch < 1)
         return jt::fail(JT_ERR_INVALID, "samples/bounces must be >= 0 and batch >= 1");
+    if (params->bounces > 32766)  // the kernel keeps bounce in 15 bits of the path's control word
+        return jt::fail(JT_ERR_UNSUPPORTED, "bounces above 32766 are not supported");
     if (bvh->nshapes != scene->nshapes) return jt::fail(JT_ERR_INVALID, "bvh.nshapes != scene.nshapes");
     // ------------------------------------------------------------- validate what the reference can shade
     for (int s = 0; s < scene->nshapes; s++) {
