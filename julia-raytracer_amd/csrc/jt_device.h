@@ -24,8 +24,9 @@ namespace jtd {
 // BVH node, 32 B = two 16-B loads: a = (bmin.x, bmax.x, bmin.y, bmax.y), b = (bmin.z, bmax.z,
 // start bits, meta bits), each axis's slab planes side by side. meta = num | axis << 16 |
 // internal << 24. TLAS nodes come first (breadth-first), then every BLAS; `start` is a global
-// node index (internal), a triangle-pair / quad record slot (BLAS leaf) or a tlas_prims index
-// (TLAS leaf).
+// node index (internal), a triangle-pair / quad record slot (BLAS leaf) or, for a TLAS leaf, its
+// first instance: the device numbers instances in TLAS leaf order (bvh.primitives[i] of the
+// reference becomes instance i), so a leaf's instances are start .. start+num-1.
 struct alignas(16) DNode {
     float4 a, b;
 };
@@ -94,7 +95,6 @@ struct alignas(16) DLight {
 
 struct DScene {
     const DNode* nodes;      // TLAS nodes, then every BLAS (global node indices)
-    const int* tlas_prims;  // instance ids in leaf order
     const float4* prims;  // triangle pair: 5 float4 (p1, p2-p1, p3-p1 of two triangles interleaved,
                           // then both element ids); quad: 4 float4 (p1|elem, p2, p3, p4|p3==p4)
     const DInstTrav* inst_trav;
@@ -136,7 +136,7 @@ struct DScene {
     int ovf_stride;
     int ring;  // entries of the LDS ring in use (a power of two <= the kernel's RING)
     int stack_need;  // stack bound of the scene: LDS-mode kernels without overflow allocate this many
-    int o_nodes, o_tlas_prims, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
+    int o_nodes, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
     int o_pos, o_nrm, o_tc, o_col, o_elems, o_materials, o_lights, o_cdf, o_enrm, o_enrm_id;
 };
 

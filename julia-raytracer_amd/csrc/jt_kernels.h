@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "jt_bsdf.h"
 #include "jt_device.h"
@@ -321,7 +322,21 @@ __device__ __forceinline__ Hit query_hit(const Trav& T) {
 
 __device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T.nprim > 0; }
 
-__device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d, unsigned root, int* stack) {
+// Stack entries: 32 bits (type << 30 | snap << 24 | index) in the HBM-mode kernels; 16 bits in the
+// LDS-mode kernels without overflow (type << 14 | index: the LDS-mode scene holds fewer than 2^14
+// nodes and instances, jt_create checks; no snapshot), which halves their stack's LDS.
+__device__ __forceinline__ void st_store(int* s, unsigned e) { *s = (int)e; }
+__device__ __forceinline__ void st_store(unsigned short* s, unsigned e) {
+    *s = (unsigned short)(((e >> 16) & 0xc000u) | (e & 0x3fffu));
+}
+__device__ __forceinline__ unsigned st_load(const int* s) { return (unsigned)*s; }
+__device__ __forceinline__ unsigned st_load(const unsigned short* s) {
+    const unsigned v = *s;
+    return ((v & 0xc000u) << 16) | SNAP_NONE | (v & 0x3fffu);
+}
+
+template <class SE>
+__device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d, unsigned root, SE* stack) {
     T.wo = o;
     T.wd = d;
     T.wdinv = V3(jl_rcp(d.x), jl_rcp(d.y), jl_rcp(d.z));  // ray_dinv (src/bvh.jl:322), no guard
@@ -340,7 +355,7 @@ __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d
     T.cur_kind = KIND_TRI;
     T.inst_space = 0;
     T.negmask = neg_mask(d, S.order_flip);
-    stack[0] = (int)root;
+    st_store(stack, root);
     T.sp = 1;
     T.low = 0;
 }
@@ -407,8 +422,8 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     T.nprim -= 1;
 }
 
-template <int RING, bool OVF>
-__device__ __forceinline__ void st_push(const DScene& S, Trav& T, int* stack, int pixel, unsigned e) {
+template <int RING, bool OVF, class SE>
+__device__ __forceinline__ void st_push(const DScene& S, Trav& T, SE* stack, int pixel, unsigned e) {
     if (OVF) {
         if (T.sp - T.low == S.ring) {  // ring full: the oldest entry moves to HBM
             S.ovf[(size_t)pixel * S.ovf_stride + T.low] = stack[(T.low & (S.ring - 1)) * BLOCK];
@@ -416,12 +431,12 @@ __device__ __forceinline__ void st_push(const DScene& S, Trav& T, int* stack, in
         }
         stack[(T.sp & (S.ring - 1)) * BLOCK] = (int)e;
     } else {
-        stack[T.sp * BLOCK] = (int)e;
+        st_store(stack + T.sp * BLOCK, e);
     }
     T.sp += 1;
 }
-template <int RING, bool OVF>
-__device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* stack, int pixel) {
+template <int RING, bool OVF, class SE>
+__device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const SE* stack, int pixel) {
     T.sp -= 1;
     if (OVF) {
         // the ring slot is read unconditionally (its address is always valid; a relaxed atomic
@@ -436,15 +451,15 @@ __device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* 
         }
         return r;
     }
-    return (unsigned)stack[T.sp * BLOCK];
+    return st_load(stack + T.sp * BLOCK);
 }
 
 // Pop one stack entry: an instance entry or a TLAS/BLAS node. An instance visit and the box
 // test of its BLAS root are one step: the reference's instance visit pushes nothing but the
 // root (src/bvh.jl:345-351, 502-506), which is then the very next pop, so testing it in the same
 // step visits the same nodes in the same order.
-template <int RING, bool OVF, int COUNT, bool NCACHE, int F>
-__device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
+template <int RING, bool OVF, int COUNT, bool NCACHE, int F, class SE>
+__device__ __forceinline__ void node_step(const DScene& S, Trav& T, SE* stack, int pixel, Counters& cnt) {
     // without FT_XFORM every instance ray is the world ray: no transform, no space switch
     constexpr bool XF = (F & FT_XFORM) != 0;
     const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
@@ -515,7 +530,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         }
     } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
         for (int k = num - 1; k >= 0; k--)
-            st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | SNAP_NONE | (unsigned)S.tlas_prims[start + k]);
+            st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | SNAP_NONE | (unsigned)(start + k));
     } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
@@ -594,22 +609,65 @@ enum : int { F_HIT = 1, F_VOLUME = 2 };
 //   bits 0-14 bounce (jt_create rejects bounces > 32766), 15-22 opbounce (<= 129),
 //   23-24 flags (F_HIT, F_VOLUME), 25-31 lcount (the light-query chain, < 100).
 constexpr unsigned CTL_BOUNCE = 0x7fffu, CTL_OPB = 15, CTL_FLAGS = 23, CTL_LC = 25;
+// Parked path state (JT_PARK): the radiance sum, the light chain's shading position and the
+// nocaustics roughness bound are read only in the shading code, so they live in LDS slots of
+// the lane (pk[k * BLOCK], after the running means) instead of registers kept live across the
+// traversal loop — where the compiler spilled them to scratch (written back every shading phase).
+#ifndef JT_PARK
+#define JT_PARK 1
+#endif
+constexpr int PARK_SLOTS = 7;  // radiance xyz, lq xyz, max_roughness
+__host__ __device__ constexpr bool park(int F) { return JT_PARK != 0; }
 struct Path {
     v3 o, d;                    // pending ray (during PH_LIGHT the light query's: origin / incoming)
-    v3 radiance, weight;  // during PH_LIGHT weight already holds weight .* f (src/trace.jl:386)
+    v3 radiance_, weight;  // during PH_LIGHT weight already holds weight .* f (src/trace.jl:386)
     Rng rng;
     unsigned ctl;  // bounce | opbounce | flags | lcount (CTL_*)
     int phase;
-    float max_roughness;
+    float max_roughness_;
+    float* pk;  // the lane's parked slots (park(F))
     // sample_lights_pdf in flight (src/trace.jl:1010-1084)
     int li;
+    template <int F>
+    __device__ __forceinline__ v3 radiance() const {
+        return park(F) ? V3(pk[0], pk[BLOCK], pk[2 * BLOCK]) : radiance_;
+    }
+    template <int F>
+    __device__ __forceinline__ void set_radiance(v3 v) {
+        if (park(F)) {
+            pk[0] = v.x;
+            pk[BLOCK] = v.y;
+            pk[2 * BLOCK] = v.z;
+        } else {
+            radiance_ = v;
+        }
+    }
+    template <int F>
+    __device__ __forceinline__ v3 lq() const { return park(F) ? V3(pk[3 * BLOCK], pk[4 * BLOCK], pk[5 * BLOCK]) : lq_; }
+    template <int F>
+    __device__ __forceinline__ void set_lq(v3 v) {
+        if (park(F)) {
+            pk[3 * BLOCK] = v.x;
+            pk[4 * BLOCK] = v.y;
+            pk[5 * BLOCK] = v.z;
+        } else {
+            lq_ = v;
+        }
+    }
+    template <int F>
+    __device__ __forceinline__ float max_roughness() const { return park(F) ? pk[6 * BLOCK] : max_roughness_; }
+    template <int F>
+    __device__ __forceinline__ void set_max_roughness(float v) {
+        if (park(F)) pk[6 * BLOCK] = v;
+        else max_roughness_ = v;
+    }
     __device__ __forceinline__ int bounce() const { return (int)(ctl & CTL_BOUNCE); }
     __device__ __forceinline__ int opbounce() const { return (int)((ctl >> CTL_OPB) & 0xffu); }
     __device__ __forceinline__ bool flag(int f) const { return (ctl >> CTL_FLAGS) & (unsigned)f; }
     __device__ __forceinline__ void set_flag(int f) { ctl |= (unsigned)f << CTL_FLAGS; }
     __device__ __forceinline__ void clear_flag(int f) { ctl &= ~((unsigned)f << CTL_FLAGS); }
     __device__ __forceinline__ int lcount() const { return (int)(ctl >> CTL_LC); }
-    v3 lq;       // during PH_LIGHT: the shading position (st.o holds the light query's origin,
+    v3 lq_;      // during PH_LIGHT: the shading position (st.o holds the light query's origin,
                  // next_position of src/trace.jl:1039, so every query's ray is (st.o, st.d))
     float pb;    // sample_bsdfcos_pdf / sample_scattering_pdf
     float pdf, lpdf;
@@ -647,7 +705,7 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
     for (;;) {
         st.li += 1;
         if (st.li >= S.nlights) {
-            st.o = st.lq;  // the next bounce's ray starts at the shading position
+            st.o = st.lq<F>();  // the next bounce's ray starts at the shading position
             const float pdf = st.pdf * S.light_pick_pdf;  // sample_uniform_pdf(nlights), host-computed
             st.weight = st.weight / (0.5f * st.pb + 0.5f * pdf);  // (weight .* f) / (...)
             return after_weight(P, st);
@@ -656,7 +714,7 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
         if (l.instance >= 0) {
             st.lpdf = 0.0f;
             st.ctl &= (1u << CTL_LC) - 1u;  // lcount = 0
-            st.o = st.lq;  // the first query starts at the shading position
+            st.o = st.lq<F>();  // the first query starts at the shading position
             st.phase = PH_LIGHT;
             return false;
         }
@@ -667,7 +725,7 @@ template <int F>
 __device__ __forceinline__ bool begin_light_pdf(const DScene& S, const DParams& P, Path& st) {
     st.pdf = 0.0f;
     st.li = -1;
-    st.lq = st.o;
+    st.set_lq<F>(st.o);
     return light_advance<F>(S, P, st);
 }
 // one intersect_instance_bvh result of the instance-light loop (src/trace.jl:1024-1044)
@@ -678,7 +736,7 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
         v3 lposition = eval_position<F>(S, l.instance, h.elem, V2(h.u, h.v));
         v3 lnormal = eval_element_normal(S, l.instance, h.elem);
         const float area = S.cdf[l.cdf_offset + l.ncdf - 1];
-        v3 dd = lposition - st.lq;
+        v3 dd = lposition - st.lq<F>();
         st.lpdf += dot(dd, dd) / (__builtin_fabsf(dot(lnormal, st.d)) * area);
         st.o = lposition + st.d * 0.001f;
         st.ctl += 1u << CTL_LC;  // lcount += 1 (< 100: fits its 7 bits)
@@ -709,11 +767,13 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
 #define JT_LANE_LDS_NONE 1
 #endif
 __host__ __device__ constexpr bool lane_lds(int F) { return JT_LANE_LDS && (F != FT_NONE || JT_LANE_LDS_NONE); }
-constexpr int ACC_SLOTS = JT_LANE_LDS ? 13 : 11;  // the host sizes LDS for the larger layout
+constexpr int ACC_SLOTS = (JT_LANE_LDS ? 13 : 11) + (JT_PARK ? PARK_SLOTS : 0);  // the host sizes LDS for the larger layout
 // Lane-LDS slots: [11] the lane's sample index, [12] its running-mean weight. The FT_NONE
 // kernels (JT_LANE_LDS_NONE) recompute the weight from the sample index instead of storing it:
 // with 12 slots cornellbox's LDS-mode workgroup still fits 5 per CU.
-__host__ __device__ constexpr int acc_slots(int F) { return lane_lds(F) ? (F == FT_NONE ? 12 : 13) : 11; }
+__host__ __device__ constexpr int acc_base_slots(int F) { return lane_lds(F) ? (F == FT_NONE ? 12 : 13) : 11; }
+// + the parked path state (JT_PARK, Path::pk = acc + acc_base_slots(F) * BLOCK)
+__host__ __device__ constexpr int acc_slots(int F) { return acc_base_slots(F) + (park(F) ? PARK_SLOTS : 0); }
 struct Aov {
     float* acc;
     float w_;    // !lane_lds(F)
@@ -742,7 +802,8 @@ template <int F, class AovT>
 __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const AovT& aov,
                                          unsigned& shades) {
     if (!isec.hit) {
-        if (st.bounce() > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
+        if (st.bounce() > 0 || !P.envhidden)
+            st.set_radiance<F>(st.radiance<F>() + st.weight * eval_environment<F>(S, st.d));
         return true;
     }
     bool in_volume = false;
@@ -761,8 +822,8 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
         eval_shading<F>(S, isec.inst, isec.elem, V2(isec.u, isec.v), outgoing, sh);
         shades++;
         if (P.nocaustics) {
-            st.max_roughness = jl_max(sh.mat.roughness, st.max_roughness);
-            sh.mat.roughness = st.max_roughness;
+            st.set_max_roughness<F>(jl_max(sh.mat.roughness, st.max_roughness<F>()));
+            sh.mat.roughness = st.max_roughness<F>();
         }
         if ((F & FT_OPAC) && sh.mat.opacity < 1 && rand1f(st.rng) >= sh.mat.opacity) {
             if (st.opbounce() > 128) return true;
@@ -774,7 +835,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
             st.set_flag(F_HIT);
             aov_update<F>(aov, sh.mat.color, sh.normal);
         }
-        st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
+        st.set_radiance<F>(st.radiance<F>() + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0)));
         v3 incoming;
         const bool delta = is_delta(sh.mat);
         if (!delta) {
@@ -840,7 +901,8 @@ template <int F, class AovT>
 __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Path& st, Hit isec, const AovT& aov,
                                           unsigned& shades) {
     if (!isec.hit) {
-        if (st.bounce() > 0 || !P.envhidden) st.radiance = st.radiance + st.weight * eval_environment<F>(S, st.d);
+        if (st.bounce() > 0 || !P.envhidden)
+            st.set_radiance<F>(st.radiance<F>() + st.weight * eval_environment<F>(S, st.d));
         return true;
     }
     v3 outgoing = -st.d;
@@ -857,7 +919,7 @@ __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Pat
         st.set_flag(F_HIT);
         aov_update<F>(aov, sh.mat.color, sh.normal);
     }
-    st.radiance = st.radiance + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0));
+    st.set_radiance<F>(st.radiance<F>() + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0)));
     v3 incoming, f;
     float p;
     if (sh.mat.roughness != 0) {
@@ -904,6 +966,7 @@ __device__ __forceinline__ void eval_camera(const DCamera& cam, v2 image_uv, v2 
 }
 
 // trace_sample prologue (src/trace.jl:597-608): 4 draws, camera ray (sample_camera :651-674)
+template <int F>
 __device__ __forceinline__ void start_path(const DParams& P, int i, int j, int pixel, int sample, Path& st) {
     st.rng = rng_init(P.seed, pixel, sample);
     v2 puv = rand2f(st.rng);
@@ -918,9 +981,9 @@ __device__ __forceinline__ void start_path(const DParams& P, int i, int j, int p
         uv = V2(((float)i + fuv.x) / (float)P.width, ((float)j + fuv.y) / (float)P.height);
     }
     eval_camera(P.cam, uv, P.cam.pinhole ? sample_disk_signs(luv) : sample_disk(luv), st.o, st.d);
-    st.radiance = V3(0, 0, 0);
+    st.set_radiance<F>(V3(0, 0, 0));
     st.weight = V3(1, 1, 1);
-    st.max_roughness = 0.0f;
+    st.set_max_roughness<F>(0.0f);
     st.ctl = 0u;  // bounce 0 (the first loop iteration: -1 + 1; bounces >= 0 always enters), no flags
     st.phase = PH_SCENE;
 }
@@ -1002,9 +1065,9 @@ __device__ __forceinline__ int opaque_lane_id() {
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
 // mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, class SE>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
-                                           int* stack) {
+                                           SE* stack) {
     const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0};
     // Paths, scene rays and light queries are counted per wave, never in per-lane registers
@@ -1080,13 +1143,14 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         aov.w_ = 1.0f / (float)(sample - P.first + 1);
     }
     Path st;
+    st.pk = acc + acc_base_slots(F) * BLOCK;
     Trav T;
     // lane states, from the stack cursor alone: sp < 0 finished (no samples left), nprim > 0 or
     // sp > 0 in a query, sp == nprim == 0 waiting for the shading phase
     T.sp = -1;
     T.nprim = 0;
     if (alive) {
-        start_path(P, i, j, pixel, sample, st);
+        start_path<F>(P, i, j, pixel, sample, st);
         query_begin(S, T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
     }
     if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(alive));
@@ -1197,7 +1261,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 // trace_sample epilogue (src/trace.jl:625-648)
                 if (WC) c_path = true;
                 else lds_count(0, true);
-                v3 radiance = st.radiance;
+                v3 radiance = st.radiance<F>();
                 if (!all_finite(radiance)) radiance = V3(0, 0, 0);
                 const float mr = max3(radiance);
                 if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
@@ -1225,7 +1289,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                     if (F != FT_NONE) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
                     const int lx = opaque_lane_id();
                     const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
-                    start_path(P, i2, j2, j2 * P.width + i2, sample, st);
+                    start_path<F>(P, i2, j2, j2 * P.width + i2, sample, st);
                 }
                 } else {
                 if (++sample >= cs1) {
@@ -1233,7 +1297,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                     T.sp = -1;
                 } else {
                     aov.w_ = 1.0f / (float)(sample - P.first + 1);
-                    start_path(P, i, j, pixel, sample, st);
+                    start_path<F>(P, i, j, pixel, sample, st);
                 }
                 }
             }
@@ -1333,11 +1397,16 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #define JT_WAVES_PER_EU
 #define JT_WAVES_PER_EU_F(F)
 #endif
+// LDS-mode stack bytes per workgroup: a RING-entry 32-bit ring with HBM overflow, else the scene's
+// bound in 16-bit entries (rounded to 16 B: the blob follows)
+__host__ __device__ constexpr size_t lds_stack_bytes(bool ovf, int ring, int need) {
+    return ovf ? (size_t)ring * BLOCK * 4 : ((size_t)need * BLOCK * 2 + 15) / 16 * 16;
+}
+
 // the scene arrays of the LDS blob (small-scene mode; offsets from jt_create)
 __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob) {
     DScene L = S;
     L.nodes = reinterpret_cast<const DNode*>(blob + S.o_nodes);
-    L.tlas_prims = reinterpret_cast<const int*>(blob + S.o_tlas_prims);
     L.prims = reinterpret_cast<const float4*>(blob + S.o_prims);
     L.inst_trav = reinterpret_cast<const DInstTrav*>(blob + S.o_inst_trav);
     L.inst_blas = reinterpret_cast<const int4*>(blob + S.o_inst_blas);
@@ -1369,11 +1438,13 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, 
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     extern __shared__ uint4 dyn_lds[];
-    uint4* blob = dyn_lds + ((OVF ? RING : S.stack_need) * BLOCK) / 4;  // the stack takes the first entries
+    // the stack takes the first bytes (16-bit entries without overflow: lds_stack_bytes), the blob follows
+    uint4* blob = dyn_lds + lds_stack_bytes(OVF, RING, S.stack_need) / 16;
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
     const DScene L = blob_scene(S, blob);
-    trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+    using SE = std::conditional_t<OVF, int, unsigned short>;
+    trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<SE*>(dyn_lds) + threadIdx.x);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of
@@ -1388,7 +1459,7 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
     hipError_t e;
     if constexpr (LDSK) {
         if (S.blob_n16 > 0) {
-        const size_t lds = (size_t)(OVF ? RING : S.stack_need) * BLOCK * 4 + (size_t)S.blob_n16 * 16;
+        const size_t lds = lds_stack_bytes(OVF, RING, S.stack_need) + (size_t)S.blob_n16 * 16;
         const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>;
         if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;

@@ -352,6 +352,15 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     }
     int st = check_tree(bvh->tlas, scene->ninstances, "tlas");
     if (st != JT_OK) return st;
+    // the device numbers instances in TLAS leaf order (a leaf's instances are then the id range
+    // start .. start+num-1, no per-instance index load): the TLAS must list each instance once
+    std::vector<int> inst_new(scene->ninstances, -1);  // reference instance id -> device id
+    for (int k = 0; k < bvh->tlas.nprimitives; k++) {
+        int& slot = inst_new[bvh->tlas.primitives[k]];
+        if (slot >= 0) return jt::fail(JT_ERR_INVALID, "tlas: an instance is listed twice");
+        slot = k;
+    }
+    if (st != JT_OK) return st;
     int max_blas_depth = 0;
     for (int s = 0; s < scene->nshapes; s++) {
         const jt_shape& sh = scene->shapes[s];
@@ -433,7 +442,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             tlas[q] = pack_node(n, n.internal ? newidx[n.start] : n.start);
         }
     }
-    std::vector<int> tlas_prims(bvh->tlas.primitives, bvh->tlas.primitives + bvh->tlas.nprimitives);
     std::vector<DNode> blas;
     std::vector<float4> prims;
     std::vector<DShape> shapes(scene->nshapes);
@@ -558,8 +566,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     std::vector<DInstTrav> itrav(scene->ninstances);
     std::vector<int4> iblas(scene->ninstances);
     std::vector<DInstShade> ishade(scene->ninstances);
-    for (int k = 0; k < scene->ninstances; k++) {
-        const jt_instance& in = scene->instances[k];
+    for (int k0 = 0; k0 < scene->ninstances; k0++) {  // k0: the reference's id, k: the device's
+        const int k = inst_new[k0];
+        const jt_instance& in = scene->instances[k0];
         jt::frame3 f = jt::load_frame(in.frame);
         jt::frame3 inv = jt::inverse_frame(f, true);
         float iv[12], fv[12];
@@ -645,7 +654,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     c->env_alias = env_alias;
     for (int k = 0; k < lights->nlights; k++) {
         const jt_light& l = lights->lights[k];
-        dl[k] = DLight{l.instance, l.environment, (int)cdf.size(), l.ncdf, 0, 0, 0.0f, -1};
+        dl[k] = DLight{l.instance >= 0 ? inst_new[l.instance] : -1, l.environment, (int)cdf.size(), l.ncdf, 0, 0, 0.0f, -1};
         cdf.insert(cdf.end(), l.cdf, l.cdf + l.ncdf);
         const float last = l.ncdf > 0 ? l.cdf[l.ncdf - 1] : 0.0f;
         bool monotone = true;
@@ -680,7 +689,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     // traversal stack entries carry a 24-bit node / instance index (IDX_MASK)
     if (nodes.size() > IDX_MASK || (size_t)scene->ninstances > IDX_MASK)
         return bail(jt::fail(JT_ERR_UNSUPPORTED, "scene exceeds 2^24 BVH nodes or instances"));
-    if ((st = upload(c, nodes, &S.nodes)) || (st = upload(c, tlas_prims, &S.tlas_prims)) || (st = upload(c, prims, &S.prims)) ||
+    if ((st = upload(c, nodes, &S.nodes)) || (st = upload(c, prims, &S.prims)) ||
         (st = upload(c, itrav, &S.inst_trav)) || (st = upload(c, iblas, &S.inst_blas)) || (st = upload(c, ishade, &S.inst_shade)) ||
         (st = upload(c, shapes, &S.shapes)) || (st = upload(c, pos, &S.pos)) || (st = upload(c, nrm, &S.nrm)) ||
         (st = upload(c, tc, &S.tc)) || (st = upload(c, col, &S.col)) || (st = upload(c, elems, &S.elems)) ||
@@ -708,7 +717,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             return off;
         };
         S.o_nodes = add(nodes.data(), nodes.size() * sizeof(DNode));
-        S.o_tlas_prims = add(tlas_prims.data(), tlas_prims.size() * sizeof(int));
         S.o_prims = add(prims.data(), prims.size() * sizeof(float4));
         S.o_inst_trav = add(itrav.data(), itrav.size() * sizeof(DInstTrav));
         S.o_inst_blas = add(iblas.data(), iblas.size() * sizeof(int4));
@@ -734,13 +742,15 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         // overflow, just the scene's bound
         const size_t acc_bytes = (size_t)ACC_SLOTS * BLOCK * 4;
         const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 4 + acc_bytes;
-        const size_t lds_base = (size_t)(c->stack <= 16 ? c->stack : c->ring) * BLOCK * 4 + acc_bytes;
+        const size_t lds_base = lds_stack_bytes(c->stack > 16, c->ring, c->stack) + acc_bytes;
         const size_t bytes = blob.size() * 16;
         const size_t lds_cu = 160 * 1024;
         const size_t wg_hbm = std::min<size_t>(4, lds_cu / base_bytes), wg_lds = lds_cu / (lds_base + bytes);
         S.blob = nullptr;
         S.blob_n16 = 0;
-        if (bytes <= budget && wg_lds >= wg_hbm) {
+        // LDS-mode kernels without overflow keep 16-bit stack entries: 14-bit node / instance ids
+        const bool ids16 = c->stack > 16 || (nodes.size() < (1u << 14) && (size_t)scene->ninstances < (1u << 14));
+        if (bytes <= budget && wg_lds >= wg_hbm && ids16) {
             std::vector<uint4> b(blob);
             if ((st = upload(c, b, &S.blob))) return bail(st);
             S.blob_n16 = (int)blob.size();
