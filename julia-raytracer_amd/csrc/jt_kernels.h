@@ -23,7 +23,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <type_traits>
 
 #include "jt_bsdf.h"
 #include "jt_device.h"
@@ -322,21 +321,7 @@ __device__ __forceinline__ Hit query_hit(const Trav& T) {
 
 __device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T.nprim > 0; }
 
-// Stack entries: 32 bits (type << 30 | snap << 24 | index) in the HBM-mode kernels; 16 bits in the
-// LDS-mode kernels without overflow (type << 14 | index: the LDS-mode scene holds fewer than 2^14
-// nodes and instances, jt_create checks; no snapshot), which halves their stack's LDS.
-__device__ __forceinline__ void st_store(int* s, unsigned e) { *s = (int)e; }
-__device__ __forceinline__ void st_store(unsigned short* s, unsigned e) {
-    *s = (unsigned short)(((e >> 16) & 0xc000u) | (e & 0x3fffu));
-}
-__device__ __forceinline__ unsigned st_load(const int* s) { return (unsigned)*s; }
-__device__ __forceinline__ unsigned st_load(const unsigned short* s) {
-    const unsigned v = *s;
-    return ((v & 0xc000u) << 16) | SNAP_NONE | (v & 0x3fffu);
-}
-
-template <class SE>
-__device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d, unsigned root, SE* stack) {
+__device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d, unsigned root, int* stack) {
     T.wo = o;
     T.wd = d;
     T.wdinv = V3(jl_rcp(d.x), jl_rcp(d.y), jl_rcp(d.z));  // ray_dinv (src/bvh.jl:322), no guard
@@ -355,7 +340,7 @@ __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d
     T.cur_kind = KIND_TRI;
     T.inst_space = 0;
     T.negmask = neg_mask(d, S.order_flip);
-    st_store(stack, root);
+    stack[0] = (int)root;
     T.sp = 1;
     T.low = 0;
 }
@@ -422,8 +407,8 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     T.nprim -= 1;
 }
 
-template <int RING, bool OVF, class SE>
-__device__ __forceinline__ void st_push(const DScene& S, Trav& T, SE* stack, int pixel, unsigned e) {
+template <int RING, bool OVF>
+__device__ __forceinline__ void st_push(const DScene& S, Trav& T, int* stack, int pixel, unsigned e) {
     if (OVF) {
         if (T.sp - T.low == S.ring) {  // ring full: the oldest entry moves to HBM
             S.ovf[(size_t)pixel * S.ovf_stride + T.low] = stack[(T.low & (S.ring - 1)) * BLOCK];
@@ -431,12 +416,12 @@ __device__ __forceinline__ void st_push(const DScene& S, Trav& T, SE* stack, int
         }
         stack[(T.sp & (S.ring - 1)) * BLOCK] = (int)e;
     } else {
-        st_store(stack + T.sp * BLOCK, e);
+        stack[T.sp * BLOCK] = (int)e;
     }
     T.sp += 1;
 }
-template <int RING, bool OVF, class SE>
-__device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const SE* stack, int pixel) {
+template <int RING, bool OVF>
+__device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const int* stack, int pixel) {
     T.sp -= 1;
     if (OVF) {
         // the ring slot is read unconditionally (its address is always valid; a relaxed atomic
@@ -451,15 +436,15 @@ __device__ __forceinline__ unsigned st_pop(const DScene& S, Trav& T, const SE* s
         }
         return r;
     }
-    return st_load(stack + T.sp * BLOCK);
+    return (unsigned)stack[T.sp * BLOCK];
 }
 
 // Pop one stack entry: an instance entry or a TLAS/BLAS node. An instance visit and the box
 // test of its BLAS root are one step: the reference's instance visit pushes nothing but the
 // root (src/bvh.jl:345-351, 502-506), which is then the very next pop, so testing it in the same
 // step visits the same nodes in the same order.
-template <int RING, bool OVF, int COUNT, bool NCACHE, int F, class SE>
-__device__ __forceinline__ void node_step(const DScene& S, Trav& T, SE* stack, int pixel, Counters& cnt) {
+template <int RING, bool OVF, int COUNT, bool NCACHE, int F>
+__device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
     // without FT_XFORM every instance ray is the world ray: no transform, no space switch
     constexpr bool XF = (F & FT_XFORM) != 0;
     const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
@@ -616,8 +601,14 @@ constexpr unsigned CTL_BOUNCE = 0x7fffu, CTL_OPB = 15, CTL_FLAGS = 23, CTL_LC = 
 #ifndef JT_PARK
 #define JT_PARK 1
 #endif
-constexpr int PARK_SLOTS = 7;  // radiance xyz, lq xyz, max_roughness
-__host__ __device__ constexpr bool park(int F) { return JT_PARK != 0; }
+constexpr int PARK_SLOTS = 7;  // radiance xyz, max_roughness, lq xyz
+// slots: [0, 3) radiance, 3 max_roughness, [4, 7) lq. The mesh kernels park (features2 +6 %,
+// bathroom1 +14 %, ecosys +9 %: their spills fell from 12-28 to 0-7 VGPRs). The FT_NONE kernel
+// (cornellbox, 2-8 spilled VGPRs either way) does not: its light-hit steps read the light-chain
+// position every few traversal iterations, and parking cost 4-11 % there (profiles/r03_park/).
+__host__ __device__ constexpr bool park(int F) { return JT_PARK != 0 && F != FT_NONE; }
+__host__ __device__ constexpr bool park_lq(int F) { return park(F); }
+__host__ __device__ constexpr int park_slots(int F) { return park(F) ? PARK_SLOTS : 0; }
 struct Path {
     v3 o, d;                    // pending ray (during PH_LIGHT the light query's: origin / incoming)
     v3 radiance_, weight;  // during PH_LIGHT weight already holds weight .* f (src/trace.jl:386)
@@ -643,22 +634,22 @@ struct Path {
         }
     }
     template <int F>
-    __device__ __forceinline__ v3 lq() const { return park(F) ? V3(pk[3 * BLOCK], pk[4 * BLOCK], pk[5 * BLOCK]) : lq_; }
+    __device__ __forceinline__ v3 lq() const { return park_lq(F) ? V3(pk[4 * BLOCK], pk[5 * BLOCK], pk[6 * BLOCK]) : lq_; }
     template <int F>
     __device__ __forceinline__ void set_lq(v3 v) {
-        if (park(F)) {
-            pk[3 * BLOCK] = v.x;
-            pk[4 * BLOCK] = v.y;
-            pk[5 * BLOCK] = v.z;
+        if (park_lq(F)) {
+            pk[4 * BLOCK] = v.x;
+            pk[5 * BLOCK] = v.y;
+            pk[6 * BLOCK] = v.z;
         } else {
             lq_ = v;
         }
     }
     template <int F>
-    __device__ __forceinline__ float max_roughness() const { return park(F) ? pk[6 * BLOCK] : max_roughness_; }
+    __device__ __forceinline__ float max_roughness() const { return park(F) ? pk[3 * BLOCK] : max_roughness_; }
     template <int F>
     __device__ __forceinline__ void set_max_roughness(float v) {
-        if (park(F)) pk[6 * BLOCK] = v;
+        if (park(F)) pk[3 * BLOCK] = v;
         else max_roughness_ = v;
     }
     __device__ __forceinline__ int bounce() const { return (int)(ctl & CTL_BOUNCE); }
@@ -773,7 +764,7 @@ constexpr int ACC_SLOTS = (JT_LANE_LDS ? 13 : 11) + (JT_PARK ? PARK_SLOTS : 0); 
 // with 12 slots cornellbox's LDS-mode workgroup still fits 5 per CU.
 __host__ __device__ constexpr int acc_base_slots(int F) { return lane_lds(F) ? (F == FT_NONE ? 12 : 13) : 11; }
 // + the parked path state (JT_PARK, Path::pk = acc + acc_base_slots(F) * BLOCK)
-__host__ __device__ constexpr int acc_slots(int F) { return acc_base_slots(F) + (park(F) ? PARK_SLOTS : 0); }
+__host__ __device__ constexpr int acc_slots(int F) { return acc_base_slots(F) + park_slots(F); }
 struct Aov {
     float* acc;
     float w_;    // !lane_lds(F)
@@ -1065,9 +1056,9 @@ __device__ __forceinline__ int opaque_lane_id() {
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
 // mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, class SE>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
-                                           SE* stack) {
+                                           int* stack) {
     const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0};
     // Paths, scene rays and light queries are counted per wave, never in per-lane registers
@@ -1397,10 +1388,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #define JT_WAVES_PER_EU
 #define JT_WAVES_PER_EU_F(F)
 #endif
-// LDS-mode stack bytes per workgroup: a RING-entry 32-bit ring with HBM overflow, else the scene's
-// bound in 16-bit entries (rounded to 16 B: the blob follows)
+// LDS-mode stack bytes per workgroup: a RING-entry ring with HBM overflow, else the scene's bound
 __host__ __device__ constexpr size_t lds_stack_bytes(bool ovf, int ring, int need) {
-    return ovf ? (size_t)ring * BLOCK * 4 : ((size_t)need * BLOCK * 2 + 15) / 16 * 16;
+    return (size_t)(ovf ? ring : need) * BLOCK * 4;
 }
 
 // the scene arrays of the LDS blob (small-scene mode; offsets from jt_create)
@@ -1438,13 +1428,12 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, 
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     extern __shared__ uint4 dyn_lds[];
-    // the stack takes the first bytes (16-bit entries without overflow: lds_stack_bytes), the blob follows
+    // the stack takes the first bytes (lds_stack_bytes), the blob follows
     uint4* blob = dyn_lds + lds_stack_bytes(OVF, RING, S.stack_need) / 16;
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
     const DScene L = blob_scene(S, blob);
-    using SE = std::conditional_t<OVF, int, unsigned short>;
-    trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<SE*>(dyn_lds) + threadIdx.x);
+    trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of

@@ -748,9 +748,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         const size_t wg_hbm = std::min<size_t>(4, lds_cu / base_bytes), wg_lds = lds_cu / (lds_base + bytes);
         S.blob = nullptr;
         S.blob_n16 = 0;
-        // LDS-mode kernels without overflow keep 16-bit stack entries: 14-bit node / instance ids
-        const bool ids16 = c->stack > 16 || (nodes.size() < (1u << 14) && (size_t)scene->ninstances < (1u << 14));
-        if (bytes <= budget && wg_lds >= wg_hbm && ids16) {
+        if (bytes <= budget && wg_lds >= wg_hbm) {
             std::vector<uint4> b(blob);
             if ((st = upload(c, b, &S.blob))) return bail(st);
             S.blob_n16 = (int)blob.size();
