@@ -98,7 +98,7 @@ struct DScene {
     const float4* prims;  // triangle pair: 5 float4 (p1, p2-p1, p3-p1 of two triangles interleaved,
                           // then both element ids); quad: 4 float4 (p1|elem, p2, p3, p4|p3==p4)
     const DInstTrav* inst_trav;
-    const int4* inst_blas;  // per instance: blas_root, kind, identity-transform flag, shape
+    const int4* inst_blas;  // per instance: blas_root, identity-transform flag, kind, shape
     const DInstShade* inst_shade;
     const DShape* shapes;
     const float4* pos;

@@ -53,6 +53,24 @@ using namespace jtd;
 
 
 // ============================================================================ scene evaluation
+// One 16-B row of a record, loaded whole for every lane that reaches it. Without the pin the
+// compiler narrows a record load to the fields each path reads, and fields read on different
+// paths (or at non-adjacent offsets) become several smaller loads. On gfx950 a gather costs one
+// vector-memory wave-instruction whatever its width up to 16 B and whatever the number of active
+// lanes (scripts/td_width_bench.hip, scripts/td_lanes_bench.hip), and the HBM-mode kernels are
+// bound by exactly those instructions. Only the kernels with scene features pin (F != FT_NONE):
+// cornellbox's LDS-mode kernel reads these records from LDS.
+template <int F>
+__device__ __forceinline__ int4 row16(const void* p) {
+    int4 v = *reinterpret_cast<const int4*>(p);
+    if (F != FT_NONE) __asm__("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+    return v;
+}
+// row 3 of DInstShade: material, shape, mat_type, rot_identity
+template <int F>
+__device__ __forceinline__ int4 inst_ids(const DScene& S, int inst) {
+    return row16<F>(reinterpret_cast<const char*>(S.inst_shade + inst) + 48);
+}
 __device__ __forceinline__ fr3 inst_frame(const DScene& S, int inst) {
     const DInstShade& r = S.inst_shade[inst];
     return frame_from(r.f0, r.f1, r.f2);
@@ -62,23 +80,26 @@ __device__ __forceinline__ fr3 inst_frame(const DScene& S, int inst) {
 template <int F>
 __device__ __forceinline__ v3 eval_position(const DScene& S, int inst, int elem, v2 uv) {
     const DInstShade& is = S.inst_shade[inst];
-    const DShape sh = S.shapes[is.shape];
-    const int4 e = S.elems[sh.idx_base + elem];
+    const int4 sh = row16<F>(S.shapes + inst_ids<F>(S, inst).y);  // DShape row 0: kind, .., idx_base
+    const int4 e = S.elems[sh.w + elem];
     const fr3 f = frame_from(is.f0, is.f1, is.f2);
     v3 p1 = xyz(S.pos[e.x]), p2 = xyz(S.pos[e.y]), p3 = xyz(S.pos[e.z]);
-    if (!(F & FT_QUAD) || sh.kind == KIND_TRI) return transform_point(f, interp_tri(p1, p2, p3, uv));
+    if (!(F & FT_QUAD) || sh.x == KIND_TRI) return transform_point(f, interp_tri(p1, p2, p3, uv));
     return transform_point(f, interp_quad(p1, p2, p3, xyz(S.pos[e.w]), uv));
 }
 // eval_element_normal (src/scene.jl:578-612): transform_normal(frame, triangle/quad normal),
 // with the element normal (and, for an unrotated frame, the whole result) precomputed
-__device__ __forceinline__ v3 element_normal(const DScene& S, const DInstShade& is, const fr3& f, int g) {
-    if (is.rot_identity) return xyz(S.enrm_id[g]);
-    return transform_normal(f, xyz(S.enrm[g]));
+// (one load from either array, selected per lane: lanes of both kinds share the instruction)
+__device__ __forceinline__ v3 element_normal(const DScene& S, int rot_identity, const fr3& f, int g) {
+    const v3 n = xyz((rot_identity ? S.enrm_id : S.enrm)[g]);
+    return rot_identity ? n : transform_normal(f, n);
 }
+template <int F>
 __device__ __forceinline__ v3 eval_element_normal(const DScene& S, int inst, int elem) {
     const DInstShade& is = S.inst_shade[inst];
-    const DShape sh = S.shapes[is.shape];
-    return element_normal(S, is, frame_from(is.f0, is.f1, is.f2), sh.idx_base + elem);
+    const int4 ids = inst_ids<F>(S, inst);
+    const int4 sh = row16<F>(S.shapes + ids.y);
+    return element_normal(S, ids.w, frame_from(is.f0, is.f1, is.f2), sh.w + elem);
 }
 // eval_normal (src/scene.jl:525-576)
 __device__ __forceinline__ v3 eval_normal(const DScene& S, const DShape& sh, const int4& e, const fr3& f, v2 uv) {
@@ -203,7 +224,7 @@ __device__ __forceinline__ void eval_shading(const DScene& S, int inst, int elem
     if ((F & FT_TEX) && m.normal_tex >= 0) {
         normal = eval_normalmap(S, sh, e, f, m, uv);
     } else if (!(F & FT_ATTR) || sh.nrm_base < 0) {
-        normal = element_normal(S, is, f, sh.idx_base + elem);
+        normal = element_normal(S, is.rot_identity, f, sh.idx_base + elem);
     } else {
         normal = eval_normal(S, sh, e, f, uv);
     }
@@ -451,8 +472,8 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
     unsigned type = e >> 30, idx = e & IDX_MASK;
     if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
         if (COUNT) cnt.instances++;
-        const int4 ib = S.inst_blas[idx];  // blas_root, kind, identity, shape
-        if (!XF || ib.z) {
+        const int4 ib = S.inst_blas[idx];  // blas_root, identity, kind, shape (one load: x, y adjacent)
+        if (!XF || ib.y) {
             // inverse(identity) is exactly the identity: transform_ray returns the ray bit for bit
             if (XF && T.inst_space) world_ray(S, T);
         } else {
@@ -465,7 +486,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             T.inst_space = 1;
         }
         T.cur_inst = (int)idx;
-        T.cur_kind = ib.y;
+        T.cur_kind = ib.z;
         type = T_BLAS;
         idx = (unsigned)ib.x;
     } else if (XF && type == T_TLAS && T.inst_space) {
@@ -476,11 +497,24 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
     // HBM mode: a child pre-tested at its parent with the tmax it still has (no hit since: its
     // snapshot equals the hit count) passes this pop's box test too — same ray, same box, same
     // tmax — so only its start/meta half is loaded
+    // The second half (z slab, start/meta) is one load for every lane, the first half only for
+    // lanes that test the box: a gather costs one vector-memory wave-instruction whatever the
+    // number of active lanes (scripts/td_lanes_bench.hip), so loads shared by both kinds of pop
+    // are issued once per step instead of once per kind.
     const unsigned snap = (e >> 24) & 63u;
     float4 nb;
-    if (NCACHE && snap != 63u && snap == (unsigned)T.nh) {
+    if (NCACHE) {
+        // The second half (z slab, start/meta) is one load for every lane, the first half only
+        // for lanes that test the box: a gather costs one vector-memory wave-instruction whatever
+        // the number of active lanes (scripts/td_lanes_bench.hip), so a load shared by both kinds
+        // of pop is issued once per step instead of once per kind (bathroom1 +3 %, ecosys +2.8 %).
         nb = S.nodes[idx].b;
-    } else {
+        // keep it one 16-B load: without this the compiler narrows it to the start/meta half and
+        // sinks the z-slab half into the branch below (a second instruction in every mixed step)
+        __asm__("" : "+v"(nb.x), "+v"(nb.y), "+v"(nb.z), "+v"(nb.w));
+        if (snap == 63u || snap != (unsigned)T.nh)
+            if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, S.nodes[idx].a, nb)) return;
+    } else {  // LDS mode (no pre-test): the whole node, two LDS reads
         const DNode nd = S.nodes[idx];
         if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, nd.a, nd.b)) return;
         nb = nd.b;
@@ -723,10 +757,10 @@ __device__ __forceinline__ bool begin_light_pdf(const DScene& S, const DParams& 
 template <int F>
 __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Path& st, const Hit& h) {
     if (h.hit) {
-        const DLight l = S.lights[st.li];
-        v3 lposition = eval_position<F>(S, l.instance, h.elem, V2(h.u, h.v));
-        v3 lnormal = eval_element_normal(S, l.instance, h.elem);
-        const float area = S.cdf[l.cdf_offset + l.ncdf - 1];
+        const int4 l = row16<F>(S.lights + st.li);  // DLight row 0: instance, environment, cdf_offset, ncdf
+        v3 lposition = eval_position<F>(S, l.x, h.elem, V2(h.u, h.v));
+        v3 lnormal = eval_element_normal<F>(S, l.x, h.elem);
+        const float area = S.cdf[l.z + l.w - 1];
         v3 dd = lposition - st.lq<F>();
         st.lpdf += dot(dd, dd) / (__builtin_fabsf(dot(lnormal, st.d)) * area);
         st.o = lposition + st.d * 0.001f;

@@ -582,7 +582,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         const float idm[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
         bool ident = true;
         for (int q = 0; q < 12; q++) ident = ident && iv[q] == idm[q];
-        iblas[k] = make_int4(d.blas_root, d.kind, ident ? 1 : 0, in.shape);
+        iblas[k] = make_int4(d.blas_root, ident ? 1 : 0, d.kind, in.shape);  // jtk::node_step reads x, y (z)
         if (!ident) c->feat |= FT_XFORM;
         ishade[k] = DInstShade{f4(fv[0], fv[1], fv[2], fv[3]), f4(fv[4], fv[5], fv[6], fv[7]), f4(fv[8], fv[9], fv[10], fv[11]),
                                in.material, in.shape, scene->materials[in.material].type,
