@@ -57,7 +57,10 @@ enum : int {
     FT_VOL = 64,   // refractive / subsurface / volumetric materials (the volume stack)
     FT_XFORM = 128,  // instances whose inverse frame is not exactly the identity
     FT_NONE = 0,
-    FT_ALL = 255
+    FT_ALL = 255,
+    // kernel build flag, not a scene feature: light-hit steps in a kernel with environments
+    // (light_steps, jt_kernels.h)
+    FT_LSTEP_ENV = 4096
 };
 struct alignas(16) DShape {
     int kind, blas_root, prim_base, idx_base;

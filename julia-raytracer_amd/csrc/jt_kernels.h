@@ -620,7 +620,18 @@ __device__ __forceinline__ float env_light_pdf(const DScene& S, const DLight l, 
 // query (PH_SCENE) or one intersect_instance_bvh query of sample_lights_pdf (PH_LIGHT) —
 // which the traversal phase then advances (node_step / prim_step). Float operations and RNG draws happen
 // in exactly the reference's order; only where the lane waits between them changes.
-enum : int { PH_SCENE = 0, PH_LIGHT = 1, PH_FINISH = 2 };  // PH_FINISH: path done, sample not yet accumulated
+// PH_FINISH: path done, sample not yet accumulated; PH_ENVPDF: a light-hit step reached an
+// environment light of sample_lights_pdf, whose pdf term the shading phase adds
+enum : int { PH_SCENE = 0, PH_LIGHT = 1, PH_FINISH = 2, PH_ENVPDF = 3 };
+// Light-hit steps (trace_body) run in the path-sampler kernels without environments, and in
+// environment kernels built with FT_LSTEP_ENV: there a light-hit step stops at an environment
+// light and leaves its pdf term (env_light_pdf: atan2, acos and a CDF lookup) to the shading
+// phase, so the step stays short. Measured: features2 +13 %; in ecosys, which has no instance
+// light (no light-hit step ever runs), the code alone cost 3.4 % (spills 4 -> 7 VGPRs), so its
+// kernel is built without it (kernel_mask).
+__host__ __device__ constexpr bool light_steps(int sampler, int F) {
+    return sampler == 1 && (!(F & FT_ENV) || (F & FT_LSTEP_ENV));
+}
 enum : int { F_HIT = 1, F_VOLUME = 2 };
 
 // The path's small counters share one register (they are read only in the shading code, and as
@@ -725,7 +736,7 @@ __device__ __forceinline__ bool after_weight(const DParams& P, Path& st) {
 }
 // walk the light list: environment terms are added in place, an instance light starts its
 // query chain; after the last light the one-sample MIS weight is applied (src/trace.jl:386-397)
-template <int F>
+template <int F, bool DEFER = false>
 __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P, Path& st) {
     for (;;) {
         st.li += 1;
@@ -743,7 +754,14 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
             st.phase = PH_LIGHT;
             return false;
         }
-        if ((F & FT_ENV) && l.environment >= 0) st.pdf += env_light_pdf(S, l, st.d);
+        if ((F & FT_ENV) && l.environment >= 0) {
+            if (DEFER) {  // resumed at this light by the shading phase (PH_ENVPDF)
+                st.li -= 1;
+                st.phase = PH_ENVPDF;
+                return false;
+            }
+            st.pdf += env_light_pdf(S, l, st.d);
+        }
     }
 }
 template <int F>
@@ -754,7 +772,7 @@ __device__ __forceinline__ bool begin_light_pdf(const DScene& S, const DParams& 
     return light_advance<F>(S, P, st);
 }
 // one intersect_instance_bvh result of the instance-light loop (src/trace.jl:1024-1044)
-template <int F>
+template <int F, bool DEFER = false>
 __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Path& st, const Hit& h) {
     if (h.hit) {
         const int4 l = row16<F>(S.lights + st.li);  // DLight row 0: instance, environment, cdf_offset, ncdf
@@ -768,7 +786,7 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
         if (st.lcount() < 100) return false;
     }
     st.pdf += st.lpdf;
-    return light_advance<F>(S, P, st);
+    return light_advance<F, DEFER>(S, P, st);
 }
 
 // trace_path's bounce body after the closest-hit query (src/trace.jl:298-453)
@@ -1192,7 +1210,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         // a lane whose sample_lights_pdf query has finished does not wait for the shading
         // phase — once enough such lanes gather (or nothing else is left to step) the wave runs
         // light_hit on them and their next query starts at once.
-        constexpr bool LSTEP = SAMPLER == 1 && !(F & FT_ENV);
+        constexpr bool LSTEP = light_steps(SAMPLER, F);
+        constexpr bool LDEFER = LSTEP && (F & FT_ENV);  // environment pdf terms wait for the shading phase
         for (;;) {
             const bool wantp = T.nprim > 0;
             const bool wantn = T.nprim == 0 && T.sp > 0;
@@ -1207,12 +1226,14 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
                     bool c_lq = false, c_ray = false;
                     if (wantl) {
-                        if (light_hit<F>(S, P, st, query_hit(T))) {
+                        if (light_hit<F, LDEFER>(S, P, st, query_hit(T))) {
                             st.phase = PH_FINISH;
                         } else if (st.phase == PH_LIGHT) {
                             if (WC) c_lq = true;
                             else lds_count(2, true);
                             query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
+                        } else if (LDEFER && st.phase == PH_ENVPDF) {
+                            // waits for the shading phase (no query)
                         } else {
                             if (WC) c_ray = true;
                             else lds_count(1, true);
@@ -1268,6 +1289,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (light) done = light_hit<F>(S, P, st, query_hit(T));
             unsigned long long s1 = __builtin_amdgcn_s_memtime();
             if (LSTEP && st.phase == PH_FINISH) done = true;
+            else if (LDEFER && st.phase == PH_ENVPDF) done = light_advance<F>(S, P, st);
             else if (!light) {
                 if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
                 else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
@@ -1278,6 +1300,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (__ballot(done)) n_fin++;
 #else
             if (LSTEP && st.phase == PH_FINISH) done = true;
+            else if (LDEFER && st.phase == PH_ENVPDF) done = light_advance<F>(S, P, st);  // from its env light
             else if (light) done = light_hit<F>(S, P, st, query_hit(T));
             else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
             else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
@@ -1504,13 +1527,15 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
 // (ecosys), plus quads (features2).
 constexpr int FT_MESH = FT_TEX | FT_ATTR | FT_MAT | FT_OPAC | FT_XFORM;
 constexpr int FT_MESH_ENV = FT_MESH | FT_ENV;
-constexpr int FT_MESH_ENV_QUAD = FT_MESH_ENV | FT_QUAD;
-// the kernel mask a scene with feature bits `feat` runs with (the smallest compiled superset)
-inline int kernel_mask(int feat, int need, int ring, bool lds) {
+constexpr int FT_MESH_ENV_QUAD = FT_MESH_ENV | FT_QUAD | FT_LSTEP_ENV;
+// the kernel mask a scene with feature bits `feat` runs with (the smallest compiled superset;
+// FT_LSTEP_ENV is a build flag, not a feature). A scene with instance lights skips FT_MESH_ENV,
+// built without light-hit steps, for the next superset, which has them.
+inline int kernel_mask(int feat, int need, int ring, bool lds, bool inst_light) {
     if (need <= 16) return feat == FT_NONE ? FT_NONE : FT_ALL;
     if (ring > 16 || lds) return FT_ALL;
     for (int m : {FT_MESH, FT_MESH_ENV, FT_MESH_ENV_QUAD})
-        if (!(feat & ~m)) return m;
+        if (!(feat & ~m) && !(m == FT_MESH_ENV && inst_light)) return m;
     return FT_ALL;
 }
 

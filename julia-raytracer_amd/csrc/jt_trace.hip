@@ -818,8 +818,10 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     if (const char* cm = std::getenv("JT_CHUNK_MIN")) c->chunk_min = std::max(0, std::atoi(cm));
     // measured best (cornellbox): 40 waiting lanes per shading phase; 48 with
     // light-hit steps in the traversal phase (they take the light queries out of the phases)
-    c->kmask = kernel_mask(c->feat, c->stack, c->ring, c->lds_scene_bytes > 0);
-    const bool lstep = c->sampler != JT_SAMPLER_NAIVE && !(c->kmask & FT_ENV);  // LSTEP in trace_body
+    bool inst_light = false;  // sample_lights_pdf runs instance queries (light-hit steps can run)
+    for (int k = 0; k < lights->nlights; k++) inst_light |= lights->lights[k].instance >= 0;
+    c->kmask = kernel_mask(c->feat, c->stack, c->ring, c->lds_scene_bytes > 0, inst_light);
+    const bool lstep = light_steps(c->sampler == JT_SAMPLER_NAIVE ? 2 : 1, c->kmask) && inst_light;
     // deep BVHs (stack bound > 32: bathroom1, ecosys) shade sooner: their lanes finish queries far
     // apart, so waiting for many leaves the wave idle (measured: bathroom1 48 -> 32 +5 %, ecosys
     // 40 -> 16 +15 %; features2 and cornellbox keep 40 / 56)
@@ -962,7 +964,25 @@ namespace {
 // enqueue one launch over global samples [s0, s1) whose running-mean weight is 1/(s - first + 1)
 int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
     c->P.first = first;
-    c->P.chunk = c->chunk > 0 ? c->chunk : std::max(8, std::min(64, (s1 - s0) / 4));
+    // Samples per work unit. LDS mode (small scenes): a quarter of the launch within [8, 64].
+    // HBM mode: as long as keeps >= 32 units per resident wave, up to 256 samples — a wave waits
+    // for its slowest lane at the end of every unit, and a longer unit makes that tail a smaller
+    // share (measured at the configs' own spp: bathroom1 1024 spp 64 -> 256 +2.6 %, ecosys 64 spp
+    // 16 -> 64 +3.2 %, features2 512 spp 64 -> 128 even, 256 -1.7 %: too few units per wave;
+    // profiles/r03_loads/chunk.txt). Results do not depend on the chunking.
+    const int nsamp = s1 - s0;
+    if (c->chunk > 0) {
+        c->P.chunk = c->chunk;
+    } else if (c->lds_scene_bytes > 0) {
+        c->P.chunk = std::max(8, std::min(64, nsamp / 4));
+    } else {
+        const long long waves = (long long)std::max(1, c->cus) * 16;  // 4 workgroups of 4 waves per CU
+        const long long tiles = (c->tiles + c->P.tile_stride - 1) / c->P.tile_stride;
+        const double target = std::max(8.0, (double)nsamp * (double)tiles / (double)(waves * 32));
+        // equal chunks: the nearest count of chunks per tile, at least enough for 256 samples each
+        const int nch = std::max({1, (int)std::lround(nsamp / target), (nsamp + 255) / 256});
+        c->P.chunk = std::max(1, (nsamp + nch - 1) / nch);
+    }
     // chunk table with a halving tail: full chunks while more than two remain, then halves down
     // to chunk_min samples, so the launch ends on short units (results do not depend on chunking)
     // Auto: LDS-mode (small-scene) launches of >= 32-sample chunks end on half chunks: +1.2 % on
