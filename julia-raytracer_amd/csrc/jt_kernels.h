@@ -41,6 +41,12 @@
 #ifndef JT_FIRST_POP
 #define JT_FIRST_POP 1
 #endif
+#ifndef JT_VOTE_P
+#define JT_VOTE_P 3
+#endif
+#ifndef JT_VOTE_N
+#define JT_VOTE_N 1
+#endif
 #ifndef JT_CHILD_PRETEST
 #define JT_CHILD_PRETEST 1
 #endif
@@ -1261,7 +1267,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 T.lo = st.o;
                 T.ld = st.d;
             }
-            if (np >= nn) {
+            if (np * JT_VOTE_P >= nn * JT_VOTE_N) {
                 if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
             } else {
                 // JT_NODE_REPEAT pops per node iteration: a lane whose next step is again a
