@@ -155,6 +155,18 @@ __device__ __forceinline__ float jl_mod1(float x) {
     float m = r == 0 ? __builtin_copysignf(r, 1.0f) : (r < 0 ? r + 1.0f : r);
     return m == 0 ? 1.0f : m;
 }
+// two horizontally adjacent 8-bit texels (i, j) and (i + 1, j) in one 8-B load (one vector-memory
+// instruction instead of two; texb carries a padding texel past its end)
+struct __attribute__((aligned(4))) TexelPair {
+    uchar4 a, b;
+};
+// The two 256-entry texel-decode LUTs (srgb_lut, then byte_lut) in LDS, filled at kernel start
+// by the kernels that evaluate textures: a texel's four channel decodes are then LDS reads, not
+// four more vector-memory gathers per texel.
+static __shared__ float tex_lut[512];
+__device__ __forceinline__ v4 decode_texel(uchar4 b, const float* lut) {
+    return V4(lut[b.x], lut[b.y], lut[b.z], tex_lut[256 + b.w]);
+}
 // eval_texture (src/scene.jl:790-834): bilinear, wrap
 __device__ __forceinline__ v4 eval_texture(const DScene& S, int tex, v2 uv, bool as_linear) {
     if (tex < 0) return V4(1, 1, 1, 1);
@@ -168,10 +180,30 @@ __device__ __forceinline__ v4 eval_texture(const DScene& S, int tex, v2 uv, bool
     int j = jl_clampi((int)__builtin_truncf(tt), 0, t.height - 1);
     int ii = (i + 1) % t.width, jj = (j + 1) % t.height;
     float u = s - (float)i, v = tt - (float)j;
-    v4 a = (lookup_texture(S, t, i, j, as_linear) * (1 - u)) * (1 - v);
-    v4 b = (lookup_texture(S, t, i, jj, as_linear) * (1 - u)) * v;
-    v4 c = (lookup_texture(S, t, ii, j, as_linear) * u) * (1 - v);
-    v4 d = (lookup_texture(S, t, ii, jj, as_linear) * u) * v;
+    v4 ta, tb, tc, td;  // texels (i, j), (i, jj), (ii, j), (ii, jj)
+    if (t.is_float) {
+        ta = lookup_texture(S, t, i, j, as_linear);
+        tb = lookup_texture(S, t, i, jj, as_linear);
+        tc = lookup_texture(S, t, ii, j, as_linear);
+        td = lookup_texture(S, t, ii, jj, as_linear);
+    } else {
+        const TexelPair r0 = *reinterpret_cast<const TexelPair*>(S.texb + t.offset + (long long)j * t.width + i);
+        const TexelPair r1 = *reinterpret_cast<const TexelPair*>(S.texb + t.offset + (long long)jj * t.width + i);
+        uchar4 c0 = r0.b, c1 = r1.b;
+        if (ii == 0) {  // right edge: the neighbour wraps to column 0
+            c0 = S.texb[t.offset + (long long)j * t.width];
+            c1 = S.texb[t.offset + (long long)jj * t.width];
+        }
+        const float* lut = tex_lut + ((as_linear && !t.linear) ? 0 : 256);
+        ta = decode_texel(r0.a, lut);
+        tb = decode_texel(r1.a, lut);
+        tc = decode_texel(c0, lut);
+        td = decode_texel(c1, lut);
+    }
+    v4 a = (ta * (1 - u)) * (1 - v);
+    v4 b = (tb * (1 - u)) * v;
+    v4 c = (tc * u) * (1 - v);
+    v4 d = (td * u) * v;
     return ((a + b) + c) + d;
 }
 // eval_normalmap (src/scene.jl:722-751) with eval_element_tangents (:851-891)
@@ -1118,6 +1150,10 @@ template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
                                            int* stack) {
     const int lane = threadIdx.x & 63;
+    if constexpr ((F & (FT_TEX | FT_ENV)) != 0) {  // the texel-decode LUTs into LDS (tex_lut)
+        for (int k = threadIdx.x; k < 512; k += BLOCK) tex_lut[k] = k < 256 ? S.srgb_lut[k] : S.byte_lut[k - 256];
+        __syncthreads();
+    }
     Counters cnt{0, 0, 0, 0};
     // Paths, scene rays and light queries are counted per wave, never in per-lane registers
     // (three VGPRs live across the traversal loop, spilled and written back every shading

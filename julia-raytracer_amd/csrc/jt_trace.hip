@@ -634,6 +634,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                 texb.push_back(make_uchar4(t.pixelsb[4 * q], t.pixelsb[4 * q + 1], t.pixelsb[4 * q + 2], t.pixelsb[4 * q + 3]));
         }
     }
+    // one padding texel: eval_texture loads texels (i, j) and (i + 1, j) as one 8-B pair, which
+    // past a texture's last texel reads one texel beyond it (and ignores it)
+    texb.push_back(make_uchar4(0, 0, 0, 0));
     std::vector<DEnv> envs(scene->nenvironments);
     for (int k = 0; k < scene->nenvironments; k++) {
         const jt_environment& en = scene->environments[k];
@@ -740,7 +743,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         if (const char* v = std::getenv("JT_LDS_SCENE")) budget = (size_t)std::atoll(v);
         // HBM mode's stack is the kernel's static ring (16 or 32 entries); LDS mode's, without
         // overflow, just the scene's bound
-        const size_t acc_bytes = (size_t)ACC_SLOTS * BLOCK * 4;
+        // + the texel-decode LUTs a texture kernel keeps in LDS (trace_body)
+        const size_t acc_bytes = (size_t)ACC_SLOTS * BLOCK * 4 + ((c->feat & FT_TEX) ? 2048 : 0);
         const size_t base_bytes = (size_t)(c->stack <= 16 ? 16 : c->ring) * BLOCK * 4 + acc_bytes;
         const size_t lds_base = lds_stack_bytes(c->stack > 16, c->ring, c->stack) + acc_bytes;
         const size_t bytes = blob.size() * 16;
