@@ -85,6 +85,12 @@ struct alignas(16) DEnv {
     float emission[3];
     int tex;
 };
+// One element of an instance light, as light_hit reads it (5 float4): its object-space vertex
+// positions p1 p2 p3 (p4 for a quad in row 4), the element normal light_hit transforms (enrm, or
+// enrm_id already final when the instance frame has no rotation), the light's area (last of its
+// CDF), the rot_identity flag and the shape kind. The same floats as the arrays they come from:
+// light_hit's results are unchanged, from 4-5 loads instead of 10.
+//   row 0: p1.xyz p2.x | row 1: p2.yz p3.xy | row 2: p3.z n.xyz | row 3: area rot kind 0 | row 4: p4.xyz 0
 struct alignas(16) DLight {
     int instance, environment, cdf_offset, ncdf;
     // guide table of a long CDF (env lights; nguide = 0: plain binary search): thresholds
@@ -120,6 +126,11 @@ struct DScene {
     const float4* texf;
     const DEnv* envs;
     const DLight* lights;
+    // light-hit records (light_hit, src/trace.jl:1024-1044): per light (instance, first record,
+    // 0, 0), and per element of an instance light's shape one 80-B record of what light_hit
+    // reads, gathered on the host (DLightElem)
+    const int4* light_hit;
+    const float4* light_elems;
     const float* cdf;
     const float* guide_t;   // DLight guide tables (thresholds / first indices)
     const int* guide_a;
@@ -141,6 +152,7 @@ struct DScene {
     int stack_need;  // stack bound of the scene: LDS-mode kernels without overflow allocate this many
     int o_nodes, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
     int o_pos, o_nrm, o_tc, o_col, o_elems, o_materials, o_lights, o_cdf, o_enrm, o_enrm_id;
+    int o_light_hit, o_light_elems;
 };
 
 struct DCamera {

@@ -813,10 +813,24 @@ __device__ __forceinline__ bool begin_light_pdf(const DScene& S, const DParams& 
 template <int F, bool DEFER = false>
 __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Path& st, const Hit& h) {
     if (h.hit) {
-        const int4 l = row16<F>(S.lights + st.li);  // DLight row 0: instance, environment, cdf_offset, ncdf
-        v3 lposition = eval_position<F>(S, l.x, h.elem, V2(h.u, h.v));
-        v3 lnormal = eval_element_normal<F>(S, l.x, h.elem);
-        const float area = S.cdf[l.z + l.w - 1];
+        // the light's element record (DLightElem): eval_position + eval_element_normal + the area
+        const int4 lh = row16<F>(S.light_hit + st.li);  // instance, first record
+        const DInstShade& is = S.inst_shade[lh.x];
+        const fr3 f = frame_from(is.f0, is.f1, is.f2);
+        const float4* r = S.light_elems + 5 * (lh.y + h.elem);
+        const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+        const v3 p1 = V3(r0.x, r0.y, r0.z), p2 = V3(r0.w, r1.x, r1.y), p3 = V3(r1.z, r1.w, r2.x);
+        const v2 uv = V2(h.u, h.v);
+        v3 lposition;
+        if (!(F & FT_QUAD) || __float_as_int(r3.z) == KIND_TRI) {
+            lposition = transform_point(f, interp_tri(p1, p2, p3, uv));
+        } else {
+            const float4 r4 = r[4];
+            lposition = transform_point(f, interp_quad(p1, p2, p3, V3(r4.x, r4.y, r4.z), uv));
+        }
+        const v3 en = V3(r2.y, r2.z, r2.w);
+        v3 lnormal = __float_as_int(r3.y) ? en : transform_normal(f, en);
+        const float area = r3.x;
         v3 dd = lposition - st.lq<F>();
         st.lpdf += dot(dd, dd) / (__builtin_fabsf(dot(lnormal, st.d)) * area);
         st.o = lposition + st.d * 0.001f;
@@ -1510,6 +1524,8 @@ __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob)
     L.enrm_id = reinterpret_cast<const float4*>(blob + S.o_enrm_id);
     L.materials = reinterpret_cast<const DMaterial*>(blob + S.o_materials);
     L.lights = reinterpret_cast<const DLight*>(blob + S.o_lights);
+    L.light_hit = reinterpret_cast<const int4*>(blob + S.o_light_hit);
+    L.light_elems = reinterpret_cast<const float4*>(blob + S.o_light_elems);
     L.cdf = reinterpret_cast<const float*>(blob + S.o_cdf);
     return L;
 }

@@ -681,6 +681,36 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             }
         }
     }
+    // light-hit records (DLightElem, jt_device.h): per instance light, one per element of its shape
+    std::vector<int4> lhit(std::max(1, lights->nlights), make_int4(-1, 0, 0, 0));
+    std::vector<float4> lelems;
+    for (int k = 0; k < lights->nlights; k++) {
+        const int inst = dl[k].instance;
+        if (inst < 0) continue;
+        const DInstShade& is = ishade[inst];
+        const DShape& d = shapes[is.shape];
+        const jt_shape& sh = scene->shapes[is.shape];
+        const int nel = d.kind == KIND_TRI ? sh.ntriangles : sh.nquads;
+        const float area = lights->lights[k].ncdf > 0 ? lights->lights[k].cdf[lights->lights[k].ncdf - 1] : 0.0f;
+        lhit[k] = make_int4(inst, (int)(lelems.size() / 5), 0, 0);
+        for (int e = 0; e < nel; e++) {
+            const int g = d.idx_base + e;
+            const int4 v = elems[g];
+            const float4 p1 = pos[v.x], p2 = pos[v.y], p3 = pos[v.z];
+            const float4 p4 = d.kind == KIND_TRI ? f4(0, 0, 0, 0) : pos[v.w];
+            const float4 n = is.rot_identity ? enrm_id[g] : enrm[g];
+            float kind_bits, rot_bits;
+            const int kind = d.kind, rot = is.rot_identity ? 1 : 0;
+            std::memcpy(&kind_bits, &kind, 4);
+            std::memcpy(&rot_bits, &rot, 4);
+            lelems.push_back(f4(p1.x, p1.y, p1.z, p2.x));
+            lelems.push_back(f4(p2.y, p2.z, p3.x, p3.y));
+            lelems.push_back(f4(p3.z, n.x, n.y, n.z));
+            lelems.push_back(f4(area, rot_bits, kind_bits, 0));
+            lelems.push_back(f4(p4.x, p4.y, p4.z, 0));
+        }
+    }
+    if (lelems.empty()) lelems.assign(5, f4(0, 0, 0, 0));
     std::vector<float> srgb, bytes;
     build_luts(srgb, bytes);
 
@@ -698,7 +728,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, tc, &S.tc)) || (st = upload(c, col, &S.col)) || (st = upload(c, elems, &S.elems)) ||
         (st = upload(c, enrm, &S.enrm)) || (st = upload(c, enrm_id, &S.enrm_id)) ||
         (st = upload(c, mats, &S.materials)) || (st = upload(c, texs, &S.textures)) || (st = upload(c, texb, &S.texb)) ||
-        (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) ||
+        (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) || (st = upload(c, lhit, &S.light_hit)) || (st = upload(c, lelems, &S.light_elems)) ||
         (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
         return bail(st);
     S.tlas_nnodes = (int)tlas.size();
@@ -735,6 +765,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         S.o_materials = add(mats.data(), mats.size() * sizeof(DMaterial));
         S.o_lights = add(dl.data(), dl.size() * sizeof(DLight));
         S.o_cdf = add(cdf.data(), cdf.size() * sizeof(float));
+        S.o_light_hit = add(lhit.data(), lhit.size() * sizeof(int4));
+        S.o_light_elems = add(lelems.data(), lelems.size() * sizeof(float4));
         // LDS mode only when the blob does not cost workgroups per CU: the kernel holds at most
         // 4 workgroups per CU (4 waves/SIMD), so the blob + stack + accumulators may use up to
         // 160 KiB / 4, or as much as HBM mode's stack + accumulators already cost. Override
