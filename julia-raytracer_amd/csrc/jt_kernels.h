@@ -1190,6 +1190,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
     unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
     unsigned long long dead_lanes = 0;  // lanes done with their unit's samples, per traversal iteration
+    // material coherence of the shading phases (what material sorting could gain): phases with
+    // surface hits to shade, and their summed distinct material types and material ids
+    unsigned long long n_mph = 0, n_mty = 0, n_mid = 0;
 #endif
     // this launch's tiles: every tile_stride-th from tile_offset (all of them on one device)
     const int tiles_x = (P.width + 7) / 8, tiles = launch_tiles(P);
@@ -1336,6 +1339,27 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
         // shading phase: every waiting lane consumes its hit and issues its next query
         bool c_path = false, c_lq = false, c_ray = false;
+#if JT_STAMPS
+        {
+            int mid = -1, mt = -1;
+            if ((T.sp | T.nprim) == 0 && st.phase == PH_SCENE && T.h_inst >= 0) {
+                mid = S.inst_shade[T.h_inst].material;
+                mt = (F & FT_MAT) ? S.materials[mid].type : (int)M_MATTE;
+            }
+            if (__ballot(mt >= 0)) {
+                n_mph++;
+                for (int ty = 0; ty <= (int)M_GLTFPBR; ty++) n_mty += __ballot(mt == ty) ? 1u : 0u;
+                bool counted = mt < 0;
+                for (;;) {
+                    const unsigned long long m = __ballot(!counted);
+                    if (!m) break;
+                    const int v = __shfl(mid, __ffsll((long long)m) - 1);
+                    counted = counted || mid == v;
+                    n_mid++;
+                }
+            }
+        }
+#endif
         if ((T.sp | T.nprim) == 0) {
             bool alive = true;
             const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
@@ -1472,6 +1496,9 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         atomicAdd(dbg + 13, n_phit);
         atomicAdd(dbg + 14, n_fin);
         atomicAdd(dbg + 15, dead_lanes);
+        atomicAdd(dbg + 16, n_mph);
+        atomicAdd(dbg + 17, n_mty);
+        atomicAdd(dbg + 18, n_mid);
     }
 #endif
     // one atomic per counter per wave (the wave's own LDS adds precede this read in program order)

@@ -1314,10 +1314,11 @@ int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
     return JT_OK;
 }
 
-// diagnostic build only (JT_STAMPS=1): per-phase wave clocks (16 u64), read by scripts/stamps.py
+// diagnostic build only (JT_STAMPS=1): per-phase wave clocks and shading-phase material coherence
+// (19 u64), read by scripts/stamps.py
 extern "C" int jt_debug_stamps(jt_ctx* c, unsigned long long* out8) {
     if (!c || !out8) return jt::fail(JT_ERR_INVALID, "NULL argument");
-    hipError_t e = hipMemcpy(out8, c->A.counters + 8, 16 * 8, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpy(out8, c->A.counters + 8, 19 * 8, hipMemcpyDeviceToHost);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy stamps");
 }
 
