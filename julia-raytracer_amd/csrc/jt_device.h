@@ -140,6 +140,7 @@ struct DScene {
     int tlas_nnodes, nenvs, nlights;
     int order_flip;  // jt_params.traversal: 0 the reference's child order, 7 the near child first
     float light_pick_pdf;  // sample_uniform_pdf(nlights) = Float32(1 / nlights) (src/sampling.jl:31)
+    int light_inline;  // every instance light's shape BVH is one leaf: light chains run inline (jtk::light_chain)
     // Small-scene mode: every array above that the traversal and shading read per step, packed
     // in one 16-B aligned blob the workgroup copies into LDS at kernel start (offsets in 16-B
     // units; -1 = not in the blob). Texels, environments and LUTs stay in HBM.

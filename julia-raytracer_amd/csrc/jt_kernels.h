@@ -841,6 +841,27 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
     return light_advance<F, DEFER>(S, P, st);
 }
 
+// The light chain of sample_lights_pdf run inline (DScene::light_inline: every instance light's
+// shape BVH is one leaf): each intersect_instance_bvh (src/bvh.jl:493-520) is the instance visit
+// with its root box test (node_step) and the leaf's primitives (prim_step), then light_hit, until
+// the chain leaves its instance lights. The same functions and the same per-lane order as through
+// the traversal loop, so results and counters are unchanged; only where the lane runs them moves:
+// here, where most of the wave's lanes run their chains side by side, instead of one-prim-step
+// queries and light-hit steps of a few lanes inside the traversal phase. Returns light_hit's
+// "path done"; otherwise st.phase is the next query's (PH_SCENE) or PH_ENVPDF (DEFER).
+template <int RING, bool OVF, int COUNT, bool NCACHE, int F, bool DEFER, class CountLq>
+__device__ __forceinline__ bool light_chain(const DScene& S, const DParams& P, Path& st, Trav& T, int* stack, int pixel,
+                                            Counters& cnt, CountLq count_lq) {
+    do {
+        count_lq();
+        query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
+        node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);  // instance + its one-leaf root
+        while (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+        if (light_hit<F, DEFER>(S, P, st, query_hit(T))) return true;
+    } while (st.phase == PH_LIGHT);
+    return false;
+}
+
 // trace_path's bounce body after the closest-hit query (src/trace.jl:298-453)
 // The albedo/normal running means (src/trace.jl:635-636) are updated as soon as the bounce-0
 // surface is accepted — their targets are final at that point — so they are not path state.
@@ -1279,7 +1300,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
             int nw = lane_count(__builtin_amdgcn_ballot_w64(waiting));
             const int nb = np + nn;
-            if (LSTEP) {
+            if (LSTEP && !S.light_inline) {  // inline light chains never wait in PH_LIGHT
                 const bool wantl = waiting && st.phase == PH_LIGHT;
                 const int nl = lane_count(__builtin_amdgcn_ballot_w64(wantl));
                 if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
@@ -1339,6 +1360,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
         // shading phase: every waiting lane consumes its hit and issues its next query
         bool c_path = false, c_lq = false, c_ray = false;
+        unsigned n_inl = 0;  // WC: this lane's inline light queries (light_chain)
 #if JT_STAMPS
         {
             int mid = -1, mt = -1;
@@ -1385,6 +1407,14 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
             else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
 #endif
+            if (SAMPLER == 1 && !done && st.phase == PH_LIGHT && S.light_inline) {
+                unsigned nlq = 0;
+                done = light_chain<RING, OVF, COUNT, NCACHE, F, false>(S, P, st, T, stack, pixel, cnt, [&] {
+                    if (WC) nlq++;
+                    else lds_count(2, true);
+                });
+                if (WC) n_inl += nlq;
+            }
             if (done) {
                 // trace_sample epilogue (src/trace.jl:625-648)
                 if (WC) c_path = true;
@@ -1460,6 +1490,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             w_paths += lane_count(__builtin_amdgcn_ballot_w64(c_path));
             w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
             w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
+            if (SAMPLER == 1 && S.light_inline) w_lq += __builtin_amdgcn_readfirstlane(wave_sum(n_inl));
         }
         if (__ballot(T.sp >= 0) == 0) break;
     }

@@ -738,6 +738,23 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     S.nenvs = scene->nenvironments;
     S.nlights = lights->nlights;
     S.light_pick_pdf = lights->nlights > 0 ? (float)(1.0 / (double)lights->nlights) : 0.0f;
+    // Inline light queries: when every instance light's shape BVH is one leaf (cornellbox's and
+    // bathroom1's two-triangle lights, features2's quads), each intersect_instance_bvh of
+    // sample_lights_pdf is an instance visit, one box test and at most four primitive tests, so the
+    // lane runs its whole light chain where the chain starts (jtk::light_chain) instead of through
+    // the traversal loop. JT_LIGHT_INLINE=0 turns it off (A/B runs); results are identical.
+    {
+        bool inl = true;
+        for (int k = 0; k < lights->nlights; k++) {
+            const int i0 = lights->lights[k].instance;
+            if (i0 < 0) continue;
+            const jt_bvh_tree& t = bvh->blas[scene->instances[i0].shape];
+            inl = inl && t.nnodes > 0 && !t.nodes[0].internal;
+        }
+        const char* li = std::getenv("JT_LIGHT_INLINE");
+        if (li && std::atoi(li) == 0) inl = false;
+        S.light_inline = inl ? 1 : 0;
+    }
 
     // ------------------------------------------------------------- small-scene LDS blob
     {
@@ -1336,11 +1353,11 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     char tmp[512];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d env_alias=%d",
+                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d env_alias=%d light_inline=%d",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, c->kmask, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
                   c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->P.nct, c->tiles, BLOCK,
-                  c->env_alias ? 1 : 0);
+                  c->env_alias ? 1 : 0, c->S.light_inline);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;
 }

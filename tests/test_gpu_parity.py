@@ -177,6 +177,7 @@ def test_light_hit_steps_are_bitwise_invariant(gpu, abi, lib, cornell_abi, monke
     lights = trace.make_trace_lights(cornell_abi, lib)
     p = make_params(abi, resolution=72, samples=5, sampler=1)
     outs = []
+    monkeypatch.setenv("JT_LIGHT_INLINE", "0")  # cornellbox's light chains otherwise never leave the shading phase
     for ll in ("1", "7", "65"):
         monkeypatch.setenv("JT_LIGHT_LANES", ll)
         st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)

@@ -193,3 +193,35 @@ def test_mesh_specialisations_bitwise_equal(gpu, abi, lib, monkeypatch, name, ma
         assert np.array_equal(a, b)
     for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades"):
         assert outs[0][2][k] == outs[1][2][k], k
+
+
+@pytest.mark.parametrize("name,lds", [("cornellbox", "65536"), ("cornellbox", "0"), ("bathroom1", None),
+                                      ("features2", None), ("materials1", None)])
+def test_inline_light_chains_bitwise_equal(gpu, abi, lib, monkeypatch, name, lds):
+    """Scenes whose instance lights are one-leaf shape BVHs run sample_lights_pdf's light chain
+    inline in the shading phase (DScene::light_inline) instead of through the traversal loop and
+    its light-hit steps. The same node/primitive steps in the same per-lane order: images, AOVs
+    and every counter must be bit-identical to the traversal path (JT_LIGHT_INLINE=0), in the
+    LDS-mode FT_NONE kernel (cornellbox), its HBM mode, and the mesh kernels."""
+    from jtrace import sceneio, trace
+    sa = abi.SceneABI(sceneio.load_scene(CORNELL)) if name == "cornellbox" else scene_abi(name)
+    if lds is not None:
+        monkeypatch.setenv("JT_LDS_SCENE", lds)
+    p = make_params(abi, resolution=96, samples=3)
+    bvh = trace.make_scene_bvh(sa, False, lib)
+    lights = trace.make_trace_lights(sa, lib)
+    outs = []
+    for inl in ("1", "0"):
+        monkeypatch.setenv("JT_LIGHT_INLINE", inl)
+        st = trace.make_trace_state(sa, bvh, lights, p, lib)
+        st.set_counters(1)
+        st.trace_range(0, 3)
+        outs.append((st.get_image(), st.get_aovs(), st.counters(), st.describe()))
+        st.close()
+    assert "light_inline=1" in outs[0][3] and "light_inline=0" in outs[1][3], (outs[0][3], outs[1][3])
+    assert outs[0][2]["light_queries"] > 0
+    assert np.array_equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert np.array_equal(a, b)
+    for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades"):
+        assert outs[0][2][k] == outs[1][2][k], k
