@@ -58,10 +58,12 @@ enum : int {
     FT_XFORM = 128,  // instances whose inverse frame is not exactly the identity
     FT_NONE = 0,
     FT_ALL = 255,
-    // kernel build flag, not a scene feature: light-hit steps in a kernel with environments
-    // (light_steps, jt_kernels.h)
-    FT_LSTEP_ENV = 4096
+    // kernel build flag, not a scene feature: the scene's light chains run inline
+    // (DScene::light_inline; jt_kernels.h light_chain), so the kernel has no light-hit steps
+    FT_LINL = 8192
 };
+// a kernel mask of no scene feature (the FT_NONE kernels, with or without the FT_LINL build flag)
+__host__ __device__ constexpr bool ft_none(int F) { return (F & ~FT_LINL) == FT_NONE; }
 struct alignas(16) DShape {
     int kind, blas_root, prim_base, idx_base;
     int pos_base, nrm_base, tc_base, col_base;  // -1 = absent

@@ -64,12 +64,12 @@ using namespace jtd;
 // paths (or at non-adjacent offsets) become several smaller loads. On gfx950 a gather costs one
 // vector-memory wave-instruction whatever its width up to 16 B and whatever the number of active
 // lanes (scripts/td_width_bench.hip, scripts/td_lanes_bench.hip), and the HBM-mode kernels are
-// bound by exactly those instructions. Only the kernels with scene features pin (F != FT_NONE):
+// bound by exactly those instructions. Only the kernels with scene features pin (!ft_none(F)):
 // cornellbox's LDS-mode kernel reads these records from LDS.
 template <int F>
 __device__ __forceinline__ int4 row16(const void* p) {
     int4 v = *reinterpret_cast<const int4*>(p);
-    if (F != FT_NONE) __asm__("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+    if (!ft_none(F)) __asm__("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
     return v;
 }
 // row 3 of DInstShade: material, shape, mat_type, rot_identity
@@ -658,18 +658,17 @@ __device__ __forceinline__ float env_light_pdf(const DScene& S, const DLight l, 
 // query (PH_SCENE) or one intersect_instance_bvh query of sample_lights_pdf (PH_LIGHT) —
 // which the traversal phase then advances (node_step / prim_step). Float operations and RNG draws happen
 // in exactly the reference's order; only where the lane waits between them changes.
-// PH_FINISH: path done, sample not yet accumulated; PH_ENVPDF: a light-hit step reached an
-// environment light of sample_lights_pdf, whose pdf term the shading phase adds
-enum : int { PH_SCENE = 0, PH_LIGHT = 1, PH_FINISH = 2, PH_ENVPDF = 3 };
-// Light-hit steps (trace_body) run in the path-sampler kernels without environments, and in
-// environment kernels built with FT_LSTEP_ENV: there a light-hit step stops at an environment
-// light and leaves its pdf term (env_light_pdf: atan2, acos and a CDF lookup) to the shading
-// phase, so the step stays short. Measured: features2 +13 %; in ecosys, which has no instance
-// light (no light-hit step ever runs), the code alone cost 3.4 % (spills 4 -> 7 VGPRs), so its
-// kernel is built without it (kernel_mask).
+// PH_FINISH: path done (in a light-hit step), sample not yet accumulated
+enum : int { PH_SCENE = 0, PH_LIGHT = 1, PH_FINISH = 2 };
+// Light-hit steps (trace_body) run in the path-sampler FT_NONE kernel built without FT_LINL:
+// matte scenes whose light chains cannot run inline (a light shape BVH of more than one leaf).
+// Every other kernel either runs the chains inline (FT_LINL, or DScene::light_inline at run time)
+// or, with environments, shades light results in the shading phase.
 __host__ __device__ constexpr bool light_steps(int sampler, int F) {
-    return sampler == 1 && (!(F & FT_ENV) || (F & FT_LSTEP_ENV));
+    return sampler == 1 && !(F & FT_ENV) && !(F & FT_LINL);
 }
+// the scene's light chains run inline: known at compile time (FT_LINL) or checked at run time
+__device__ __forceinline__ bool chains_inline(int F, const DScene& S) { return (F & FT_LINL) || S.light_inline; }
 enum : int { F_HIT = 1, F_VOLUME = 2 };
 
 // The path's small counters share one register (they are read only in the shading code, and as
@@ -689,7 +688,7 @@ constexpr int PARK_SLOTS = 7;  // radiance xyz, max_roughness, lq xyz
 // bathroom1 +14 %, ecosys +9 %: their spills fell from 12-28 to 0-7 VGPRs). The FT_NONE kernel
 // (cornellbox, 2-8 spilled VGPRs either way) does not: its light-hit steps read the light-chain
 // position every few traversal iterations, and parking cost 4-11 % there (profiles/r03_park/).
-__host__ __device__ constexpr bool park(int F) { return JT_PARK != 0 && F != FT_NONE; }
+__host__ __device__ constexpr bool park(int F) { return JT_PARK != 0 && !ft_none(F); }
 __host__ __device__ constexpr bool park_lq(int F) { return park(F); }
 __host__ __device__ constexpr int park_slots(int F) { return park(F) ? PARK_SLOTS : 0; }
 struct Path {
@@ -774,7 +773,7 @@ __device__ __forceinline__ bool after_weight(const DParams& P, Path& st) {
 }
 // walk the light list: environment terms are added in place, an instance light starts its
 // query chain; after the last light the one-sample MIS weight is applied (src/trace.jl:386-397)
-template <int F, bool DEFER = false>
+template <int F>
 __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P, Path& st) {
     for (;;) {
         st.li += 1;
@@ -792,14 +791,7 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
             st.phase = PH_LIGHT;
             return false;
         }
-        if ((F & FT_ENV) && l.environment >= 0) {
-            if (DEFER) {  // resumed at this light by the shading phase (PH_ENVPDF)
-                st.li -= 1;
-                st.phase = PH_ENVPDF;
-                return false;
-            }
-            st.pdf += env_light_pdf(S, l, st.d);
-        }
+        if ((F & FT_ENV) && l.environment >= 0) st.pdf += env_light_pdf(S, l, st.d);
     }
 }
 template <int F>
@@ -810,7 +802,7 @@ __device__ __forceinline__ bool begin_light_pdf(const DScene& S, const DParams& 
     return light_advance<F>(S, P, st);
 }
 // one intersect_instance_bvh result of the instance-light loop (src/trace.jl:1024-1044)
-template <int F, bool DEFER = false>
+template <int F>
 __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Path& st, const Hit& h) {
     if (h.hit) {
         // the light's element record (DLightElem): eval_position + eval_element_normal + the area
@@ -838,7 +830,7 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
         if (st.lcount() < 100) return false;
     }
     st.pdf += st.lpdf;
-    return light_advance<F, DEFER>(S, P, st);
+    return light_advance<F>(S, P, st);
 }
 
 // The light chain of sample_lights_pdf run inline (DScene::light_inline: every instance light's
@@ -848,8 +840,8 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
 // the traversal loop, so results and counters are unchanged; only where the lane runs them moves:
 // here, where most of the wave's lanes run their chains side by side, instead of one-prim-step
 // queries and light-hit steps of a few lanes inside the traversal phase. Returns light_hit's
-// "path done"; otherwise st.phase is the next query's (PH_SCENE) or PH_ENVPDF (DEFER).
-template <int RING, bool OVF, int COUNT, bool NCACHE, int F, bool DEFER, class CountLq>
+// "path done"; otherwise st.phase is PH_SCENE (the next bounce's scene query).
+template <int RING, bool OVF, int COUNT, bool NCACHE, int F, class CountLq>
 __device__ __forceinline__ bool light_chain(const DScene& S, const DParams& P, Path& st, Trav& T, int* stack, int pixel,
                                             Counters& cnt, CountLq count_lq) {
     do {
@@ -857,7 +849,7 @@ __device__ __forceinline__ bool light_chain(const DScene& S, const DParams& P, P
         query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
         node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);  // instance + its one-leaf root
         while (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-        if (light_hit<F, DEFER>(S, P, st, query_hit(T))) return true;
+        if (light_hit<F>(S, P, st, query_hit(T))) return true;
     } while (st.phase == PH_LIGHT);
     return false;
 }
@@ -882,12 +874,12 @@ __device__ __forceinline__ bool light_chain(const DScene& S, const DParams& P, P
 #ifndef JT_LANE_LDS_NONE
 #define JT_LANE_LDS_NONE 1
 #endif
-__host__ __device__ constexpr bool lane_lds(int F) { return JT_LANE_LDS && (F != FT_NONE || JT_LANE_LDS_NONE); }
+__host__ __device__ constexpr bool lane_lds(int F) { return JT_LANE_LDS && (!ft_none(F) || JT_LANE_LDS_NONE); }
 constexpr int ACC_SLOTS = (JT_LANE_LDS ? 13 : 11) + (JT_PARK ? PARK_SLOTS : 0);  // the host sizes LDS for the larger layout
 // Lane-LDS slots: [11] the lane's sample index, [12] its running-mean weight. The FT_NONE
 // kernels (JT_LANE_LDS_NONE) recompute the weight from the sample index instead of storing it:
 // with 12 slots cornellbox's LDS-mode workgroup still fits 5 per CU.
-__host__ __device__ constexpr int acc_base_slots(int F) { return lane_lds(F) ? (F == FT_NONE ? 12 : 13) : 11; }
+__host__ __device__ constexpr int acc_base_slots(int F) { return lane_lds(F) ? (ft_none(F) ? 12 : 13) : 11; }
 // + the parked path state (JT_PARK, Path::pk = acc + acc_base_slots(F) * BLOCK)
 __host__ __device__ constexpr int acc_slots(int F) { return acc_base_slots(F) + park_slots(F); }
 struct Aov {
@@ -897,7 +889,7 @@ struct Aov {
     template <int F>
     __device__ __forceinline__ float w() const {
         if (!lane_lds(F)) return w_;
-        if (F == FT_NONE) return 1.0f / (float)(reinterpret_cast<const int*>(acc)[11 * BLOCK] - first_ + 1);
+        if (ft_none(F)) return 1.0f / (float)(reinterpret_cast<const int*>(acc)[11 * BLOCK] - first_ + 1);
         return acc[12 * BLOCK];
     }
 };
@@ -1196,7 +1188,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     // WC (mesh kernels): ballots at wave-uniform points, summed in scalar registers (bathroom1
     // +3 %, features2 +1 % over per-lane counters). The FT_NONE kernel, whose light-hit steps run
     // every few iterations, adds to three per-wave LDS words instead (ds_add, no ballot).
-    constexpr bool WC = F != FT_NONE;
+    constexpr bool WC = !ft_none(F);
     unsigned w_paths = 0, w_rays = 0, w_lq = 0;
     __shared__ unsigned wave_cnt[WC ? 1 : (BLOCK / 64) * 4];
     unsigned* const wcnt = wave_cnt + (WC ? 0 : (threadIdx.x >> 6) * 4);
@@ -1260,7 +1252,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     if (LL) {
         if (in_image) {
             acc_i[11 * BLOCK] = sample;
-            if (F != FT_NONE) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+            if (!ft_none(F)) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
         }
     } else {
         aov.w_ = 1.0f / (float)(sample - P.first + 1);
@@ -1291,7 +1283,6 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         // phase — once enough such lanes gather (or nothing else is left to step) the wave runs
         // light_hit on them and their next query starts at once.
         constexpr bool LSTEP = light_steps(SAMPLER, F);
-        constexpr bool LDEFER = LSTEP && (F & FT_ENV);  // environment pdf terms wait for the shading phase
         for (;;) {
             const bool wantp = T.nprim > 0;
             const bool wantn = T.nprim == 0 && T.sp > 0;
@@ -1300,20 +1291,18 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
             int nw = lane_count(__builtin_amdgcn_ballot_w64(waiting));
             const int nb = np + nn;
-            if (LSTEP && !S.light_inline) {  // inline light chains never wait in PH_LIGHT
+            if (LSTEP && !S.light_inline) {  // light chains run inline: none waits in PH_LIGHT
                 const bool wantl = waiting && st.phase == PH_LIGHT;
                 const int nl = lane_count(__builtin_amdgcn_ballot_w64(wantl));
                 if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
                     bool c_lq = false, c_ray = false;
                     if (wantl) {
-                        if (light_hit<F, LDEFER>(S, P, st, query_hit(T))) {
+                        if (light_hit<F>(S, P, st, query_hit(T))) {
                             st.phase = PH_FINISH;
                         } else if (st.phase == PH_LIGHT) {
                             if (WC) c_lq = true;
                             else lds_count(2, true);
                             query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
-                        } else if (LDEFER && st.phase == PH_ENVPDF) {
-                            // waits for the shading phase (no query)
                         } else {
                             if (WC) c_ray = true;
                             else lds_count(1, true);
@@ -1347,7 +1336,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 // JT_NODE_REPEAT pops per node iteration: a lane whose next step is again a
                 // stack pop takes it at once (the same steps in the same per-lane order, less
                 // per-iteration vote and loop overhead)
-                constexpr int NREP = F == FT_NONE ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
+                constexpr int NREP = ft_none(F) ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
 #pragma unroll
                 for (int k = 0; k < NREP; k++)
                     if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
@@ -1384,14 +1373,14 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
         if ((T.sp | T.nprim) == 0) {
             bool alive = true;
-            const bool light = SAMPLER == 1 && st.phase == PH_LIGHT;
+            constexpr bool LINL = (F & FT_LINL) != 0;  // no light query ever leaves the shading phase
+            const bool light = SAMPLER == 1 && !LINL && st.phase == PH_LIGHT;
             bool done;
 #if JT_STAMPS
             unsigned long long s0 = __builtin_amdgcn_s_memtime();
             if (light) done = light_hit<F>(S, P, st, query_hit(T));
             unsigned long long s1 = __builtin_amdgcn_s_memtime();
             if (LSTEP && st.phase == PH_FINISH) done = true;
-            else if (LDEFER && st.phase == PH_ENVPDF) done = light_advance<F>(S, P, st);
             else if (!light) {
                 if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
                 else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
@@ -1402,14 +1391,13 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             if (__ballot(done)) n_fin++;
 #else
             if (LSTEP && st.phase == PH_FINISH) done = true;
-            else if (LDEFER && st.phase == PH_ENVPDF) done = light_advance<F>(S, P, st);  // from its env light
             else if (light) done = light_hit<F>(S, P, st, query_hit(T));
             else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
             else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
 #endif
-            if (SAMPLER == 1 && !done && st.phase == PH_LIGHT && S.light_inline) {
+            if (SAMPLER == 1 && !done && st.phase == PH_LIGHT && chains_inline(F, S)) {
                 unsigned nlq = 0;
-                done = light_chain<RING, OVF, COUNT, NCACHE, F, false>(S, P, st, T, stack, pixel, cnt, [&] {
+                done = light_chain<RING, OVF, COUNT, NCACHE, F>(S, P, st, T, stack, pixel, cnt, [&] {
                     if (WC) nlq++;
                     else lds_count(2, true);
                 });
@@ -1444,7 +1432,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                     T.sp = -1;
                 } else {
                     acc_i[11 * BLOCK] = sample;
-                    if (F != FT_NONE) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+                    if (!ft_none(F)) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
                     const int lx = opaque_lane_id();
                     const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
                     start_path<F>(P, i2, j2, j2 * P.width + i2, sample, st);
@@ -1464,7 +1452,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             t_fin += s3 - s2;
 #endif
             if (alive) {
-                if (SAMPLER == 1 && st.phase == PH_LIGHT) {
+                if (SAMPLER == 1 && !LINL && st.phase == PH_LIGHT) {
                     if (WC) c_lq = true;
                     else lds_count(2, true);
                     query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
@@ -1490,7 +1478,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             w_paths += lane_count(__builtin_amdgcn_ballot_w64(c_path));
             w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
             w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
-            if (SAMPLER == 1 && S.light_inline) w_lq += __builtin_amdgcn_readfirstlane(wave_sum(n_inl));
+            if (SAMPLER == 1 && chains_inline(F, S)) w_lq += __builtin_amdgcn_readfirstlane(wave_sum(n_inl));
         }
         if (__ballot(T.sp >= 0) == 0) break;
     }
@@ -1554,7 +1542,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #if JT_WAVES > 0
 #define JT_WAVES_PER_EU __attribute__((amdgpu_waves_per_eu(JT_WAVES, JT_WAVES)))
 #define JT_WAVES_PER_EU_F(F) \
-    __attribute__((amdgpu_waves_per_eu((F) == FT_NONE ? JT_WAVES_NONE : JT_WAVES, (F) == FT_NONE ? JT_WAVES_NONE : JT_WAVES)))
+    __attribute__((amdgpu_waves_per_eu(ft_none(F) ? JT_WAVES_NONE : JT_WAVES, ft_none(F) ? JT_WAVES_NONE : JT_WAVES)))
 #else
 #define JT_WAVES_PER_EU
 #define JT_WAVES_PER_EU_F(F)
@@ -1640,18 +1628,21 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
 // Feature specialisations compiled per stack configuration (besides FT_ALL): FT_NONE for small
 // scenes with a 16-entry stack (cornellbox), and three masks for large HBM-mode scenes with the
 // ring + HBM overflow stack — textured, attributed meshes (bathroom1), plus environments
-// (ecosys), plus quads (features2).
+// (ecosys), plus quads (features2). FT_NONE, FT_MESH and FT_MESH_ENV_QUAD are FT_LINL builds
+// (light chains inline, no light-hit steps); a second FT_NONE build keeps the light-hit steps.
 constexpr int FT_MESH = FT_TEX | FT_ATTR | FT_MAT | FT_OPAC | FT_XFORM;
 constexpr int FT_MESH_ENV = FT_MESH | FT_ENV;
-constexpr int FT_MESH_ENV_QUAD = FT_MESH_ENV | FT_QUAD | FT_LSTEP_ENV;
-// the kernel mask a scene with feature bits `feat` runs with (the smallest compiled superset;
-// FT_LSTEP_ENV is a build flag, not a feature). A scene with instance lights skips FT_MESH_ENV,
-// built without light-hit steps, for the next superset, which has them.
-inline int kernel_mask(int feat, int need, int ring, bool lds, bool inst_light) {
-    if (need <= 16) return feat == FT_NONE ? FT_NONE : FT_ALL;
+constexpr int FT_MESH_ENV_QUAD = FT_MESH_ENV | FT_QUAD;
+// the kernel mask a scene with feature bits `feat` runs with: the smallest compiled superset.
+// `linl`: the scene's light chains can run inline (DScene::light_inline), which the FT_LINL
+// builds need; FT_MESH_ENV is built without it (the chain code cost its scenes without instance
+// lights, ecosys, 4 spilled VGPRs) and serves only scenes without instance lights. Matte scenes
+// whose chains cannot run inline get the FT_NONE build with light-hit steps.
+inline int kernel_mask(int feat, int need, int ring, bool lds, bool linl, bool inst_light) {
+    if (need <= 16) return feat == FT_NONE ? (linl ? FT_NONE | FT_LINL : FT_NONE) : FT_ALL;
     if (ring > 16 || lds) return FT_ALL;
-    for (int m : {FT_MESH, FT_MESH_ENV, FT_MESH_ENV_QUAD})
-        if (!(feat & ~m) && !(m == FT_MESH_ENV && inst_light)) return m;
+    for (int m : {FT_MESH | FT_LINL, FT_MESH_ENV, FT_MESH_ENV_QUAD | FT_LINL})
+        if (!(feat & ~m & ~FT_LINL) && ((m & FT_LINL) ? linl : !inst_light)) return m;
     return FT_ALL;
 }
 
@@ -1668,15 +1659,16 @@ struct LaunchConfig;
         static constexpr int feat = F;                    \
         static constexpr bool lds = L;                    \
     };
-JT_LAUNCH_CONFIG(0, 16, false, FT_NONE, true)            // small scenes, matte triangles (cornellbox)
+JT_LAUNCH_CONFIG(0, 16, false, FT_NONE | FT_LINL, true)  // small scenes, matte triangles (cornellbox)
 JT_LAUNCH_CONFIG(1, 16, false, FT_ALL, true)             // small scenes, any features
-JT_LAUNCH_CONFIG(2, 16, true, FT_MESH, false)            // deep BVHs: textured meshes (bathroom1)
-JT_LAUNCH_CONFIG(3, 16, true, FT_MESH_ENV, false)        // + environments (ecosys)
-JT_LAUNCH_CONFIG(4, 16, true, FT_MESH_ENV_QUAD, false)   // + quads (features2)
+JT_LAUNCH_CONFIG(2, 16, true, FT_MESH | FT_LINL, false)  // deep BVHs: textured meshes (bathroom1)
+JT_LAUNCH_CONFIG(3, 16, true, FT_MESH_ENV, false)        // + environments, no instance lights (ecosys)
+JT_LAUNCH_CONFIG(4, 16, true, FT_MESH_ENV_QUAD | FT_LINL, false)  // + quads (features2)
 JT_LAUNCH_CONFIG(5, 16, true, FT_ALL, true)              // deep BVHs, any features
 JT_LAUNCH_CONFIG(6, 32, true, FT_ALL, true)              // a 32-entry LDS ring (JT_LDS_STACK)
+JT_LAUNCH_CONFIG(7, 16, false, FT_NONE, true)            // matte triangles, light chains through the traversal
 #undef JT_LAUNCH_CONFIG
-constexpr int NUM_LAUNCH_CONFIGS = 7;
+constexpr int NUM_LAUNCH_CONFIGS = 8;
 
 template <int ID, int SAMPLER, int COUNT>
 hipError_t launch_cfg(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {

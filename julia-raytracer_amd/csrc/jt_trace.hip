@@ -28,20 +28,22 @@ JT_KV_FOR(3, extern template)
 JT_KV_FOR(4, extern template)
 JT_KV_FOR(5, extern template)
 JT_KV_FOR(6, extern template)
+JT_KV_FOR(7, extern template)
 
 // Stack configurations: the whole bound in a 16-entry LDS ring, or a RING-entry ring + HBM.
 template <int SAMPLER, int COUNT>
 hipError_t launch_s(int need, int ring, int kmask, const DScene& S, const DParams& P, int s0, int s1,
                     const DAccum& A, hipStream_t st, int cus) {
     if (need <= 16) {
-        if (kmask == FT_NONE) return launch_cfg<0, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+        if (kmask == (FT_NONE | FT_LINL)) return launch_cfg<0, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+        if (kmask == FT_NONE) return launch_cfg<7, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
         return launch_cfg<1, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
     }
     if (ring <= 16) {
         switch (kmask) {
-            case FT_MESH: return launch_cfg<2, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+            case FT_MESH | FT_LINL: return launch_cfg<2, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
             case FT_MESH_ENV: return launch_cfg<3, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
-            case FT_MESH_ENV_QUAD: return launch_cfg<4, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+            case FT_MESH_ENV_QUAD | FT_LINL: return launch_cfg<4, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
             default: return launch_cfg<5, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
         }
     }
@@ -873,13 +875,17 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     // light-hit steps in the traversal phase (they take the light queries out of the phases)
     bool inst_light = false;  // sample_lights_pdf runs instance queries (light-hit steps can run)
     for (int k = 0; k < lights->nlights; k++) inst_light |= lights->lights[k].instance >= 0;
-    c->kmask = kernel_mask(c->feat, c->stack, c->ring, c->lds_scene_bytes > 0, inst_light);
-    const bool lstep = light_steps(c->sampler == JT_SAMPLER_NAIVE ? 2 : 1, c->kmask) && inst_light;
+    c->kmask = kernel_mask(c->feat, c->stack, c->ring, c->lds_scene_bytes > 0, c->S.light_inline != 0, inst_light);
+    // light queries leave the shading phase's waiting lanes early (light-hit steps) or never wait
+    // there at all (inline chains): the gate then waits for more lanes
+    const int smp = c->sampler == JT_SAMPLER_NAIVE ? 2 : 1;
+    const bool lstep = inst_light && smp == 1 && (light_steps(smp, c->kmask) || c->S.light_inline);
     // deep BVHs (stack bound > 32: bathroom1, ecosys) shade sooner: their lanes finish queries far
-    // apart, so waiting for many leaves the wave idle (measured: bathroom1 48 -> 32 +5 %, ecosys
-    // 40 -> 16 +15 %; features2 and cornellbox keep 40 / 56)
+    // apart, so waiting for many leaves the wave idle. Measured with inline light chains
+    // (profiles/r03_inline/wl.txt): cornellbox 56, features2 56, bathroom1 40 (32: -0.8 %, 48:
+    // -1.4 %); without instance lights (ecosys) 16 (40 -> 16 was +15 %)
     const bool deep = c->stack > 32;
-    P.wait_lanes = lstep ? (c->kmask == FT_NONE && c->lds_scene_bytes ? 56 : deep ? 32 : 48) : deep ? 16 : 40;
+    P.wait_lanes = lstep ? (deep ? 40 : 56) : deep ? 16 : 40;
     if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
     P.light_lanes = 2;
     if (const char* ll = std::getenv("JT_LIGHT_LANES")) P.light_lanes = std::max(1, std::min(65, std::atoi(ll)));

@@ -11,7 +11,8 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent.parent / "julia-raytracer_amd"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
          "-DJT_EXACT_MATH=1", "-fno-slp-vectorize", "-mllvm", "-sink-insts-to-avoid-spills=1", "-DJT_WAVES=4"]
-NAMES = ["FT_NONE", "FT_ALL", "FT_MESH", "FT_MESH_ENV", "FT_MESH_ENV_QUAD", "FT_ALL ovf", "FT_ALL ring32"]
+NAMES = ["FT_NONE+LINL", "FT_ALL", "FT_MESH+LINL", "FT_MESH_ENV", "FT_MESH_ENV_QUAD+LINL", "FT_ALL ovf", "FT_ALL ring32",
+         "FT_NONE lsteps"]
 
 
 def usage(v, extra):
@@ -34,7 +35,7 @@ def usage(v, extra):
 def main():
     extra = sys.argv[1:]
     with ThreadPoolExecutor(7) as ex:
-        res = list(ex.map(lambda v: usage(v, extra), range(7)))
+        res = list(ex.map(lambda v: usage(v, extra), range(8)))
     print(f"{'config':18} {'kernel':16} {'sampler':7} {'VGPRs':>5} {'spill':>5} {'scratch':>7} {'occ':>3}")
     for v, rows in res:
         for r in rows:
