@@ -38,8 +38,15 @@
 #ifndef JT_NODE_REPEAT
 #define JT_NODE_REPEAT 3
 #endif
+// stack pops of a new query run where it is issued, in the shading phase (most lanes take part)
+// rather than in sparser traversal iterations: 1 in the FT_NONE kernels; 2 in the others, since
+// inline light chains (features2 +1.5 %, bathroom1 even; cornellbox -0.4 % with 2,
+// profiles/r03_inline/ab_fp_nr.txt)
+#ifndef JT_FIRST_POP_NONE
+#define JT_FIRST_POP_NONE 1
+#endif
 #ifndef JT_FIRST_POP
-#define JT_FIRST_POP 1
+#define JT_FIRST_POP 2
 #endif
 #ifndef JT_VOTE_P
 #define JT_VOTE_P 3
@@ -1464,7 +1471,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
                 // where most of the wave's lanes take part, rather than in a sparser traversal step
 #pragma unroll
-                for (int k = 0; k < JT_FIRST_POP; k++)
+                for (int k = 0; k < (ft_none(F) ? JT_FIRST_POP_NONE : JT_FIRST_POP); k++)
                     if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
             }
 #if JT_STAMPS
