@@ -60,10 +60,12 @@ enum : int {
     FT_ALL = 255,
     // kernel build flag, not a scene feature: the scene's light chains run inline
     // (DScene::light_inline; jt_kernels.h light_chain), so the kernel has no light-hit steps
-    FT_LINL = 8192
+    FT_LINL = 8192,
+    // kernel build flag: the scene has no instance light (sample_lights_pdf never queries a BVH)
+    FT_NOIL = 16384
 };
 // a kernel mask of no scene feature (the FT_NONE kernels, with or without the FT_LINL build flag)
-__host__ __device__ constexpr bool ft_none(int F) { return (F & ~FT_LINL) == FT_NONE; }
+__host__ __device__ constexpr bool ft_none(int F) { return (F & ~(FT_LINL | FT_NOIL)) == FT_NONE; }
 struct alignas(16) DShape {
     int kind, blas_root, prim_base, idx_base;
     int pos_base, nrm_base, tc_base, col_base;  // -1 = absent

@@ -39,9 +39,9 @@
 #define JT_NODE_REPEAT 3
 #endif
 // stack pops of a new query run where it is issued, in the shading phase (most lanes take part)
-// rather than in sparser traversal iterations: 1 in the FT_NONE kernels; 2 in the others, since
-// inline light chains (features2 +1.5 %, bathroom1 even; cornellbox -0.4 % with 2,
-// profiles/r03_inline/ab_fp_nr.txt)
+// rather than in sparser traversal iterations: 2 in the FT_LINL mesh kernels since inline light
+// chains (features2 +1.5 %, bathroom1 even; cornellbox -0.4 % with 2,
+// profiles/r03_inline/ab_fp_nr.txt), 1 in the others (ecosys lost 7 % with 2)
 #ifndef JT_FIRST_POP_NONE
 #define JT_FIRST_POP_NONE 1
 #endif
@@ -349,9 +349,10 @@ struct Counters {  // diagnostic traversal counts (COUNT=1); paths / rays / ligh
 // intersect_instance_bvh (root = one instance entry). node_step() / prim_step() do one unit of work: one
 // node (box test + push), one instance entry (ray to instance space), or ONE primitive test of
 // the current leaf (leaf cursor), so every step costs about the same whatever a lane is doing.
-// Visit order — children far-first per d[axis] sign, a TLAS leaf's instances in order, a BLAS
-// leaf's primitives in order before anything else is popped — is exactly the reference's, so
-// the closest hit and its tie-breaking (t == tmax replaces; only t > tmax rejects) match.
+// Visit order — children per d[axis] sign (far-first as the reference, or near-first with
+// JT_TRAVERSAL_NEAR), a TLAS leaf's instances in order, a BLAS leaf's primitives in order before
+// anything else is popped — is the oracle's in either mode, so the closest hit and its
+// tie-breaking (t == tmax replaces; only t > tmax rejects) match it.
 struct Trav {
     v3 wo, wd, wdinv;  // world-space ray of the query
     v3 lo, ld, ldinv;  // the ray every node test uses: the world ray, or inside a BLAS the ray
@@ -675,7 +676,7 @@ __host__ __device__ constexpr bool light_steps(int sampler, int F) {
     return sampler == 1 && !(F & FT_ENV) && !(F & FT_LINL);
 }
 // the scene's light chains run inline: known at compile time (FT_LINL) or checked at run time
-__device__ __forceinline__ bool chains_inline(int F, const DScene& S) { return (F & FT_LINL) || S.light_inline; }
+__device__ __forceinline__ bool chains_inline(int F, const DScene& S) { return !(F & FT_NOIL) && ((F & FT_LINL) || S.light_inline); }
 enum : int { F_HIT = 1, F_VOLUME = 2 };
 
 // The path's small counters share one register (they are read only in the shading code, and as
@@ -791,7 +792,7 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
             return after_weight(P, st);
         }
         const DLight l = S.lights[st.li];
-        if (l.instance >= 0) {
+        if (!(F & FT_NOIL) && l.instance >= 0) {
             st.lpdf = 0.0f;
             st.ctl &= (1u << CTL_LC) - 1u;  // lcount = 0
             st.o = st.lq<F>();  // the first query starts at the shading position
@@ -1380,7 +1381,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
         if ((T.sp | T.nprim) == 0) {
             bool alive = true;
-            constexpr bool LINL = (F & FT_LINL) != 0;  // no light query ever leaves the shading phase
+            // no light query ever leaves the shading phase (FT_LINL), or none exists (FT_NOIL)
+            constexpr bool LINL = (F & (FT_LINL | FT_NOIL)) != 0;
             const bool light = SAMPLER == 1 && !LINL && st.phase == PH_LIGHT;
             bool done;
 #if JT_STAMPS
@@ -1471,7 +1473,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
                 // where most of the wave's lanes take part, rather than in a sparser traversal step
 #pragma unroll
-                for (int k = 0; k < (ft_none(F) ? JT_FIRST_POP_NONE : JT_FIRST_POP); k++)
+                for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
                     if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
             }
 #if JT_STAMPS
@@ -1642,14 +1644,14 @@ constexpr int FT_MESH_ENV = FT_MESH | FT_ENV;
 constexpr int FT_MESH_ENV_QUAD = FT_MESH_ENV | FT_QUAD;
 // the kernel mask a scene with feature bits `feat` runs with: the smallest compiled superset.
 // `linl`: the scene's light chains can run inline (DScene::light_inline), which the FT_LINL
-// builds need; FT_MESH_ENV is built without it (the chain code cost its scenes without instance
-// lights, ecosys, 4 spilled VGPRs) and serves only scenes without instance lights. Matte scenes
+// builds need; FT_MESH_ENV is built for scenes without instance lights (FT_NOIL: no light
+// queries at all; the chain code cost ecosys 4 spilled VGPRs). Matte scenes
 // whose chains cannot run inline get the FT_NONE build with light-hit steps.
 inline int kernel_mask(int feat, int need, int ring, bool lds, bool linl, bool inst_light) {
     if (need <= 16) return feat == FT_NONE ? (linl ? FT_NONE | FT_LINL : FT_NONE) : FT_ALL;
     if (ring > 16 || lds) return FT_ALL;
-    for (int m : {FT_MESH | FT_LINL, FT_MESH_ENV, FT_MESH_ENV_QUAD | FT_LINL})
-        if (!(feat & ~m & ~FT_LINL) && ((m & FT_LINL) ? linl : !inst_light)) return m;
+    for (int m : {FT_MESH | FT_LINL, FT_MESH_ENV | FT_NOIL, FT_MESH_ENV_QUAD | FT_LINL})
+        if (!(feat & ~m & ~(FT_LINL | FT_NOIL)) && ((m & FT_LINL) ? linl : !inst_light)) return m;
     return FT_ALL;
 }
 
@@ -1669,7 +1671,7 @@ struct LaunchConfig;
 JT_LAUNCH_CONFIG(0, 16, false, FT_NONE | FT_LINL, true)  // small scenes, matte triangles (cornellbox)
 JT_LAUNCH_CONFIG(1, 16, false, FT_ALL, true)             // small scenes, any features
 JT_LAUNCH_CONFIG(2, 16, true, FT_MESH | FT_LINL, false)  // deep BVHs: textured meshes (bathroom1)
-JT_LAUNCH_CONFIG(3, 16, true, FT_MESH_ENV, false)        // + environments, no instance lights (ecosys)
+JT_LAUNCH_CONFIG(3, 16, true, FT_MESH_ENV | FT_NOIL, false)  // + environments, no instance lights (ecosys)
 JT_LAUNCH_CONFIG(4, 16, true, FT_MESH_ENV_QUAD | FT_LINL, false)  // + quads (features2)
 JT_LAUNCH_CONFIG(5, 16, true, FT_ALL, true)              // deep BVHs, any features
 JT_LAUNCH_CONFIG(6, 32, true, FT_ALL, true)              // a 32-entry LDS ring (JT_LDS_STACK)

@@ -42,7 +42,7 @@ hipError_t launch_s(int need, int ring, int kmask, const DScene& S, const DParam
     if (ring <= 16) {
         switch (kmask) {
             case FT_MESH | FT_LINL: return launch_cfg<2, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
-            case FT_MESH_ENV: return launch_cfg<3, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+            case FT_MESH_ENV | FT_NOIL: return launch_cfg<3, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
             case FT_MESH_ENV_QUAD | FT_LINL: return launch_cfg<4, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
             default: return launch_cfg<5, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
         }

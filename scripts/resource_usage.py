@@ -11,7 +11,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent.parent / "julia-raytracer_amd"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
          "-DJT_EXACT_MATH=1", "-fno-slp-vectorize", "-mllvm", "-sink-insts-to-avoid-spills=1", "-DJT_WAVES=4"]
-NAMES = ["FT_NONE+LINL", "FT_ALL", "FT_MESH+LINL", "FT_MESH_ENV", "FT_MESH_ENV_QUAD+LINL", "FT_ALL ovf", "FT_ALL ring32",
+NAMES = ["FT_NONE+LINL", "FT_ALL", "FT_MESH+LINL", "FT_MESH_ENV+NOIL", "FT_MESH_ENV_QUAD+LINL", "FT_ALL ovf", "FT_ALL ring32",
          "FT_NONE lsteps"]
 
 
