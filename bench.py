@@ -23,6 +23,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "julia-raytracer_amd"))
+from jtrace.cli import DEFAULT_TRAVERSAL  # noqa: E402  (pure Python: no torch, no library)
 
 METRIC_BASE = "Mrays/s + wall-clock render time"  # BASELINE.json metric; the workload is appended
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -103,7 +104,7 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--sampler", default="path")
     ap.add_argument("--scene", default=str(ROOT / "assets" / "scenes" / "cornellbox" / "cornellbox.json"))
-    ap.add_argument("--traversal", choices=["reference", "near"], default="near",
+    ap.add_argument("--traversal", choices=["reference", "near"], default=DEFAULT_TRAVERSAL,
                     help="BVH child order (include/jtrace.h jt_traversal): near child first (the default, the "
                          "product's order) or the reference's far-first order (src/bvh.jl:331-341)")
     ap.add_argument("--no-reference-order", action="store_true",
@@ -113,6 +114,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-spp", type=int, default=128)
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="a library run-time option (jt_set_option, include/jtrace.h) for A/B runs; repeatable")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,6 +141,9 @@ def main():
     from jtrace import abi, sceneio, trace
     from jtrace.cli import Params
     lib = abi.load_library()
+    for o in args.opt:  # A/B runs only: the driver's bench line never sets one
+        k, _, v = o.partition("=")
+        abi.set_option(lib, k, v)
     # time to first pixel, by stage (the reference's timers, src/jtrace.jl:49-65): scene load,
     # BVH build, lights, device upload (jt_create)
     t_0 = time.perf_counter()
@@ -343,6 +349,7 @@ def main():
             "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 2),
             "mlight_queries_per_s": round(agg["light_queries"] * world / elapsed / 1e6, 2),
             "time_to_first_pixel_s": ttfp,
+            "options": dict(o.partition("=")[::2] for o in args.opt) or None,
             "roofline": roof,
             "reference_order": ref_order,
             "cpu_baseline": cpu,

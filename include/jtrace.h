@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define JT_ABI_VERSION 2
+#define JT_ABI_VERSION 3  /* 2: jt_params.traversal; 3: jt_set_option */
 
 typedef enum jt_status {
     JT_OK = 0,
@@ -250,6 +250,29 @@ int jt_abi_version(void);
 const char* jt_last_error(void);
 int jt_device_count(int32_t* out);
 
+/* ---- run-time options ---------------------------------------------------------------- */
+/* Process-wide switches, read by jt_create / jt_create_multi for the contexts they create
+ * afterwards (a context keeps the values it was created with). The library never reads the
+ * environment. name, value: NUL-terminated; value NULL removes one option, name NULL (with
+ * value NULL) removes all. An unknown name fails with JT_ERR_INVALID. Unless stated, every
+ * option leaves images, AOVs and counters bit-identical to the default:
+ *   "env_alias" "1"          environment lights sample texels through alias tables (O(1)) instead
+ *                            of upper_bound: the same distribution, so results equal the default
+ *                            statistically, NOT bitwise (a variant, off by default)
+ *   "features" "all"         run the general kernel instead of the scene's specialisation
+ *   "lds_scene" "<bytes>"    budget of the small-scene LDS blob (0: scene arrays stay in HBM)
+ *   "lds_stack" "32"         a 32-entry LDS stack ring instead of 16
+ *   "light_inline" "0"       sample_lights_pdf's light queries through the traversal loop
+ *   "chunk", "chunk_min"     samples per work unit; the halving tail of the chunk table
+ *   "wait_lanes", "light_lanes"  the shading gate; the light-hit step gate
+ *   "multi_split" "tiles"|"samples"  jt_create_multi's split mode
+ * Test-only (they change WHAT is traced, for tests that reproduce a multi-device share or the
+ * stack overflow path on one GPU; jt_describe reports them when set):
+ *   "test_tiles" "k,o"       trace only the 8x8 tiles o, o + k, o + 2k, ... (one device's share of
+ *                            a k-device tile split); ignored by jt_create_multi's sample split
+ *   "test_lds_ring" "1|2|4|8|16"  use that many LDS ring entries (the rest overflow to HBM) */
+int jt_set_option(const char* name, const char* value);
+
 /* ---- host helpers (CPU only) ------------------------------------------------------- */
 /* make_scene_bvh (src/bvh.jl:66-88): one BLAS per shape (make_shape_bvh :90) and the
  * instance TLAS over transformed root boxes; split_middle (:185) or split_sah (:218). */
@@ -272,11 +295,18 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
 /* jt_create over several GPUs of one node (SURVEY §8(b) "jt_create(..., num_devices, ...)"; the
  * reference's caller is Jtrace.main's batch loop, src/jtrace.jl:83-106). devices: ndevices
  * distinct HIP ordinals, or NULL for 0 .. ndevices-1 (params->device is ignored). Every other
- * function takes the returned context: jt_trace_range / jt_trace_samples split each batch into
- * contiguous per-device shares, traced concurrently, each device keeping its own running mean
- * over its samples; jt_get_image / jt_get_aovs reduce them onto device 0 with one RCCL reduce
- * (sum of mean_d * n_d / N; hits summed), so the image equals the single-device one up to fp32
- * summation order. jt_get_counters sums the devices (kernel_ms: per launch the slowest device);
+ * function takes the returned context. Every batch is split across the devices in one of two
+ * modes, fixed at creation:
+ *   - sample split (params->batch >= ndevices): contiguous per-device shares of the batch's
+ *     samples, traced concurrently, each device keeping its own running mean over its samples;
+ *     jt_get_image / jt_get_aovs reduce them onto device 0 with one RCCL reduce whose op is a
+ *     premultiplied sum (mean_d * n_d / N; hits summed), so the image equals the single-device
+ *     one up to fp32 summation order;
+ *   - tile split (params->batch < ndevices, e.g. the reference's default --batch 1): device d
+ *     traces every sample of the batch on the interleaved 8x8 pixel tiles t with t mod ndevices
+ *     == d; the reduce is a plain sum of the disjoint tiles, bit-identical to one device.
+ * The option "multi_split" (jt_set_option: "tiles" | "samples") overrides the rule.
+ * jt_get_counters sums the devices (kernel_ms: per launch the slowest device);
  * jt_get_device_buffers returns device 0's share. */
 int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
                     const jt_params* params, const int32_t* devices, int32_t ndevices, jt_ctx** out);

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -21,6 +22,18 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 int fail(int status, const std::string& msg) {
     set_error(msg);
     return status;
+}
+
+// The run-time options of include/jtrace.h (jt_set_option). Process-wide; jt_create reads a copy.
+static std::mutex g_opt_mu;
+static std::map<std::string, std::string> g_opts;
+static const char* const kOptionNames[] = {
+    "env_alias",  "features",    "lds_scene",   "lds_stack",  "light_inline", "chunk",
+    "chunk_min",  "wait_lanes",  "light_lanes", "multi_split", "test_tiles",  "test_lds_ring",
+};
+std::map<std::string, std::string> options_snapshot() {
+    std::lock_guard<std::mutex> g(g_opt_mu);
+    return g_opts;
 }
 
 frame3 inverse_frame(const frame3& f, bool non_rigid) {
@@ -264,9 +277,30 @@ using namespace jt;
 
 extern "C" {
 
-const char* jt_version(void) { return "jtrace-mi355x 0.1 (gfx950 HIP, ABI 1)"; }
+#ifndef JT_SOURCE_HASH
+#define JT_SOURCE_HASH "unknown"
+#endif
+// ABI version and the source hash of this build (scripts/roofline.py source_hash)
+#define JT_STR2(x) #x
+#define JT_STR(x) JT_STR2(x)
+const char* jt_version(void) { return "jtrace-mi355x 0.4 (gfx950 HIP, ABI " JT_STR(JT_ABI_VERSION) ", source " JT_SOURCE_HASH ")"; }
 int jt_abi_version(void) { return JT_ABI_VERSION; }
 const char* jt_last_error(void) { return jt::g_last_error.c_str(); }
+
+int jt_set_option(const char* name, const char* value) {
+    std::lock_guard<std::mutex> g(jt::g_opt_mu);
+    if (!name) {
+        if (value) return fail(JT_ERR_INVALID, "jt_set_option: a value without a name");
+        jt::g_opts.clear();
+        return JT_OK;
+    }
+    bool known = false;
+    for (const char* k : jt::kOptionNames) known = known || std::strcmp(k, name) == 0;
+    if (!known) return fail(JT_ERR_INVALID, std::string("jt_set_option: unknown option '") + name + "'");
+    if (value) jt::g_opts[name] = value;
+    else jt::g_opts.erase(name);
+    return JT_OK;
+}
 
 static int validate_scene(const jt_scene* scene) {
     if (!scene) return fail(JT_ERR_INVALID, "scene is NULL");

@@ -3,6 +3,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <map>
 #include <string>
 
 #include "../../include/jtrace.h"
@@ -12,6 +13,10 @@ namespace jt {
 // thread-local last error (jt_last_error)
 void set_error(const std::string& msg);
 int fail(int status, const std::string& msg);
+
+// run-time options set through jt_set_option (include/jtrace.h), never read from the environment:
+// a copy of the process-wide table, taken once by jt_create / jt_create_multi
+std::map<std::string, std::string> options_snapshot();
 
 // Julia float semantics used by the host restatements (base/math.jl, Julia 1.8):
 // NaN-propagating, signbit-aware min/max; clamp = ifelse(x > hi, hi, ifelse(x < lo, lo, x)).

@@ -376,6 +376,12 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         return jt::fail(JT_ERR_STACK, "BVH deeper than --bvhstacksize (the reference throws BoundsError)");
     const int need = tlas_depth + max_blas_depth + 6;  // unified stack bound
 
+    // the run-time options (jt_set_option) this context is created with
+    const std::map<std::string, std::string> opts = jt::options_snapshot();
+    auto opt = [&](const char* k) -> const char* {
+        const auto it = opts.find(k);
+        return it == opts.end() ? nullptr : it->second.c_str();
+    };
     int32_t W = 0, H = 0;
     st = jt_image_size(scene, params, &W, &H);
     if (st != JT_OK) return st;
@@ -409,10 +415,10 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             if (sh.nnormals > 0 || sh.ntexcoords > 0 || sh.ncolors > 0) f |= FT_ATTR;
             if (sh.ncolors > 0) f |= FT_OPAC;
         }
-        const char* fe = std::getenv("JT_FEATURES");
+        const char* fe = opt("features");
         c->feat = (fe && std::strcmp(fe, "all") == 0) ? FT_ALL : f;
     }
-    if (const char* r = std::getenv("JT_LDS_STACK")) c->ring = std::atoi(r) > 16 ? 32 : 16;
+    if (const char* r = opt("lds_stack")) c->ring = std::atoi(r) > 16 ? 32 : 16;
     auto bail = [&](int status) {
         jt_destroy(c);
         return status;
@@ -654,7 +660,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     std::vector<float> cdf, guide_t;
     std::vector<int> guide_a;
     std::vector<float2> alias;
-    const char* ea = std::getenv("JT_ENV_ALIAS");
+    const char* ea = opt("env_alias");
     const bool env_alias = ea && std::atoi(ea) != 0;
     c->env_alias = env_alias;
     for (int k = 0; k < lights->nlights; k++) {
@@ -744,7 +750,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     // bathroom1's two-triangle lights, features2's quads), each intersect_instance_bvh of
     // sample_lights_pdf is an instance visit, one box test and at most four primitive tests, so the
     // lane runs its whole light chain where the chain starts (jtk::light_chain) instead of through
-    // the traversal loop. JT_LIGHT_INLINE=0 turns it off (A/B runs); results are identical.
+    // the traversal loop. Option light_inline=0 turns it off (A/B runs); results are identical.
     {
         bool inl = true;
         for (int k = 0; k < lights->nlights; k++) {
@@ -753,7 +759,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             const jt_bvh_tree& t = bvh->blas[scene->instances[i0].shape];
             inl = inl && t.nnodes > 0 && !t.nodes[0].internal;
         }
-        const char* li = std::getenv("JT_LIGHT_INLINE");
+        const char* li = opt("light_inline");
         if (li && std::atoi(li) == 0) inl = false;
         S.light_inline = inl ? 1 : 0;
     }
@@ -789,9 +795,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         // LDS mode only when the blob does not cost workgroups per CU: the kernel holds at most
         // 4 workgroups per CU (4 waves/SIMD), so the blob + stack + accumulators may use up to
         // 160 KiB / 4, or as much as HBM mode's stack + accumulators already cost. Override
-        // with JT_LDS_SCENE=0 (off) or a byte budget for the blob.
+        // with the option lds_scene=0 (off) or a byte budget for the blob.
         size_t budget = 48 * 1024;
-        if (const char* v = std::getenv("JT_LDS_SCENE")) budget = (size_t)std::atoll(v);
+        if (const char* v = opt("lds_scene")) budget = (size_t)std::atoll(v);
         // HBM mode's stack is the kernel's static ring (16 or 32 entries); LDS mode's, without
         // overflow, just the scene's bound
         // + the texel-decode LUTs a texture kernel keeps in LDS (trace_body)
@@ -814,8 +820,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     S.ovf_stride = 0;
     S.ring = c->ring;
     S.stack_need = c->stack;
-    // JT_LDS_RING (tests only): use fewer ring entries than allocated, to exercise the overflow
-    if (const char* r = std::getenv("JT_LDS_RING")) {
+    // option test_lds_ring (tests only): use fewer ring entries than allocated, to exercise the overflow
+    if (const char* r = opt("test_lds_ring")) {
         int v = std::atoi(r);
         if (v >= 1 && v <= 16 && (v & (v - 1)) == 0) {
             S.ring = v;
@@ -857,9 +863,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.seed = params->seed;
     P.tile_stride = 1;  // every tile (jt_create_multi may split by tiles)
     P.tile_offset = 0;
-    // JT_TILES=stride,offset (tests only): trace only tiles offset, offset + stride, ... — one
-    // device's share of a tile-split multi-device context, reproducible on a one-GPU box
-    if (const char* ts = std::getenv("JT_TILES")) {
+    // option test_tiles "stride,offset" (tests only): trace only tiles offset, offset + stride,
+    // ... — one device's share of a tile-split multi-device context, reproducible on one GPU
+    if (const char* ts = opt("test_tiles")) {
         int k = 0, o = 0;
         if (std::sscanf(ts, "%d,%d", &k, &o) == 2 && k >= 1 && o >= 0 && o < k) {
             P.tile_stride = k;
@@ -868,9 +874,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     }
     // lanes that must be waiting before a shading phase runs; tunable
     P.chunk = 0;  // 0: per launch, a quarter of its samples within [8, 64] (enough units per wave)
-    if (const char* ch = std::getenv("JT_CHUNK")) P.chunk = std::max(1, std::atoi(ch));
+    if (const char* ch = opt("chunk")) P.chunk = std::max(1, std::atoi(ch));
     c->chunk = P.chunk;
-    if (const char* cm = std::getenv("JT_CHUNK_MIN")) c->chunk_min = std::max(0, std::atoi(cm));
+    if (const char* cm = opt("chunk_min")) c->chunk_min = std::max(0, std::atoi(cm));
     // measured best (cornellbox): 40 waiting lanes per shading phase; 48 with
     // light-hit steps in the traversal phase (they take the light queries out of the phases)
     bool inst_light = false;  // sample_lights_pdf runs instance queries (light-hit steps can run)
@@ -887,9 +893,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     // was +15 %)
     const bool deep = c->stack > 32;
     P.wait_lanes = lstep ? (deep ? 40 : ft_none(c->kmask) ? 56 : 60) : deep ? 16 : 40;
-    if (const char* wl = std::getenv("JT_WAIT_LANES")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
+    if (const char* wl = opt("wait_lanes")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
     P.light_lanes = 2;
-    if (const char* ll = std::getenv("JT_LIGHT_LANES")) P.light_lanes = std::max(1, std::min(65, std::atoi(ll)));
+    if (const char* ll = opt("light_lanes")) P.light_lanes = std::max(1, std::min(65, std::atoi(ll)));
 
     // accumulators (make_trace_state: zeroed) + counters
     const size_t np = (size_t)W * (size_t)H;
@@ -950,17 +956,20 @@ int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lig
         c->sub.push_back(s);
     }
     c->nsub.assign(ndevices, 0);
-    // split mode (jt_ctx::tile_split); JT_MULTI_SPLIT=tiles|samples overrides
+    // split mode (jt_ctx::tile_split); the option multi_split=tiles|samples overrides
     c->tile_split = params->batch < ndevices;
-    if (const char* m = std::getenv("JT_MULTI_SPLIT")) {
-        if (std::strcmp(m, "tiles") == 0) c->tile_split = true;
-        if (std::strcmp(m, "samples") == 0) c->tile_split = false;
+    {
+        const auto opts = jt::options_snapshot();
+        const auto m = opts.find("multi_split");
+        if (m != opts.end() && m->second == "tiles") c->tile_split = true;
+        if (m != opts.end() && m->second == "samples") c->tile_split = false;
     }
-    if (c->tile_split)
-        for (int d = 0; d < ndevices; d++) {
-            c->sub[d]->P.tile_stride = ndevices;
-            c->sub[d]->P.tile_offset = d;
-        }
+    // every sub-context traces every tile under the sample split (a test_tiles option never
+    // leaves tiles out of the reduced image), its interleaved share under the tile split
+    for (int d = 0; d < ndevices; d++) {
+        c->sub[d]->P.tile_stride = c->tile_split ? ndevices : 1;
+        c->sub[d]->P.tile_offset = c->tile_split ? d : 0;
+    }
     c->comms.resize(ndevices);
     ncclResult_t r = rccl().CommInitAll(c->comms.data(), ndevices, devs.data());
     if (r != ncclSuccess) {
@@ -1349,7 +1358,7 @@ extern "C" int jt_debug_stamps(jt_ctx* c, unsigned long long* out8) {
 int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     if (!c || !buf || n <= 0) return jt::fail(JT_ERR_INVALID, "NULL argument");
     if (!c->sub.empty()) {
-        char tmp[512];
+        char tmp[640];
         const int st = jt_describe(c->sub[0], tmp, sizeof tmp);
         if (st != JT_OK) return st;
         std::snprintf(buf, (size_t)n, "%s devices=%d split=%s", tmp, (int)c->sub.size(), c->tile_split ? "tiles" : "samples");
@@ -1357,14 +1366,18 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     }
     const bool ovf = c->stack > 16;
     const int ring = ovf ? c->ring : 16;
-    char tmp[512];
+    // test-only options in effect (jt_set_option): a tile filter, a shortened LDS ring
+    char filt[96] = "";
+    if (c->P.tile_stride != 1 || c->S.ring != c->ring)
+        std::snprintf(filt, sizeof filt, " tile_filter=%d/%d ring_used=%d", c->P.tile_offset, c->P.tile_stride, c->S.ring);
+    char tmp[640];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d env_alias=%d light_inline=%d",
+                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d env_alias=%d light_inline=%d%s",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, c->kmask, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
                   c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->P.nct, c->tiles, BLOCK,
-                  c->env_alias ? 1 : 0, c->S.light_inline);
+                  c->env_alias ? 1 : 0, c->S.light_inline, filt);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;
 }

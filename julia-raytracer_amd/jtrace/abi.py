@@ -235,7 +235,8 @@ def make_params(params, camera: int = 0) -> jt_params:
     p.bvhstacksize = int(params.bvhstacksize)
     p.device = int(getattr(params, "device", 0) or 0)
     p.seed = int(getattr(params, "seed", 0x5EED))
-    p.traversal = TRAVERSAL_ORDERS.index(getattr(params, "traversal", "reference"))
+    from .cli import DEFAULT_TRAVERSAL
+    p.traversal = TRAVERSAL_ORDERS.index(getattr(params, "traversal", DEFAULT_TRAVERSAL))
     return p
 
 
@@ -253,6 +254,7 @@ def _declare(lib):
     lib.jt_abi_version.restype = C.c_int
     lib.jt_last_error.restype = C.c_char_p
     lib.jt_device_count.argtypes = [i32p]
+    lib.jt_set_option.argtypes = [C.c_char_p, C.c_char_p]
     lib.jt_build_scene_bvh.argtypes = [C.POINTER(jt_scene), C.c_int32, C.POINTER(jt_scene_bvh)]
     lib.jt_free_scene_bvh.argtypes = [C.POINTER(jt_scene_bvh)]
     lib.jt_free_scene_bvh.restype = None
@@ -283,7 +285,7 @@ def _declare(lib):
 
 # every symbol include/jtrace.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
-    "jt_version", "jt_abi_version", "jt_last_error", "jt_device_count", "jt_build_scene_bvh",
+    "jt_version", "jt_abi_version", "jt_last_error", "jt_device_count", "jt_set_option", "jt_build_scene_bvh",
     "jt_free_scene_bvh", "jt_make_lights", "jt_free_lights", "jt_image_size", "jt_create", "jt_create_multi",
     "jt_trace_samples", "jt_trace_range", "jt_get_samples", "jt_get_size", "jt_get_image",
     "jt_get_aovs", "jt_get_counters", "jt_reset", "jt_get_device_buffers", "jt_set_counters", "jt_describe", "jt_synchronize",
@@ -304,6 +306,13 @@ def load_library(path: str | os.PathLike | None = None):
     if path is None:
         _LIB = lib
     return lib
+
+
+def set_option(lib, name: str | None, value=None):
+    """jt_set_option (include/jtrace.h): a process-wide run-time option for the contexts created
+    afterwards; value None removes it, name None removes every option."""
+    check(lib, lib.jt_set_option(None if name is None else name.encode(),
+                                 None if value is None else str(value).encode()))
 
 
 def check(lib, status: int):

@@ -12,6 +12,10 @@ import argparse
 from dataclasses import dataclass
 
 SAMPLER_TYPES = ["path", "naive"]
+# BVH child visit order of every product entry point (the CLI, Params, abi.make_params, bench.py
+# and the Julia shim): near child first. "reference" is the reference's far-first order
+# (src/bvh.jl:331-341); the two differ only where two hits tie at exactly equal t.
+DEFAULT_TRAVERSAL = "near"
 
 
 def _bool(s: str) -> bool:  # ArgParse arg_type = Bool parses "true"/"false"
@@ -52,7 +56,7 @@ def _parser() -> argparse.ArgumentParser:
                    help="GPUs of this node to shard every batch over, devices 0..N-1 (extension)")
     p.add_argument("--missing", choices=["error", "drop"], default="error",
                    help="missing scene assets: error (reference) or drop (extension)")
-    p.add_argument("--traversal", choices=["reference", "near"], default="near",
+    p.add_argument("--traversal", choices=["reference", "near"], default=DEFAULT_TRAVERSAL,
                    help="BVH child order: the near child first (default), or the reference's far-first "
                         "order (extension; the images differ only where two hits tie at exactly equal t)")
     return p
@@ -84,7 +88,7 @@ class Params:
     device: int = 0
     devices: int = 1
     missing: str = "error"
-    traversal: str = "reference"
+    traversal: str = DEFAULT_TRAVERSAL
 
 
 def params_from_dict(d: dict) -> Params:

@@ -27,6 +27,7 @@ Every record carries `build`, the hash of the kernel sources and build flags it 
 usage:
   python scripts/roofline.py make --stats KT.csv --fetch DIR --write DIR [--pmc DIR] --workload W --out OUT.json
   python scripts/roofline.py check OUT.json [...]      # recompute every derived field, exit 1 on mismatch
+  python scripts/roofline.py hash                       # source_hash() of this tree (the Makefile embeds it)
 """
 from __future__ import annotations
 
@@ -43,19 +44,41 @@ HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
 # 2195.0 G lane-loads/s / 64 lanes)
 VMEM_PEAK_GIPS = 2195.0 / 64
 ROOT = __import__("pathlib").Path(__file__).resolve().parent.parent
-BUILD_FILES = ("julia-raytracer_amd/Makefile", "julia-raytracer_amd/csrc/jt_kernels.h", "julia-raytracer_amd/csrc/jt_kv.hip",
-               "julia-raytracer_amd/csrc/jt_device.h", "julia-raytracer_amd/csrc/jt_bsdf.h",
-               "julia-raytracer_amd/csrc/jt_trace.hip")
+_HIPCC_VERSION = None
+
+
+def build_files(root=ROOT):
+    """Every file the product library is built from: the Makefile, every source under csrc/ and
+    the ABI header (the Makefile's HDR set and more)."""
+    fs = ["julia-raytracer_amd/Makefile", "include/jtrace.h"]
+    fs += sorted(str(p.relative_to(root)) for p in (root / "julia-raytracer_amd" / "csrc").iterdir() if p.is_file())
+    return fs
+
+
+def hipcc_version():
+    global _HIPCC_VERSION
+    if _HIPCC_VERSION is None:
+        import subprocess
+        try:
+            out = subprocess.run(["/opt/rocm/bin/hipcc", "--version"], capture_output=True, text=True, timeout=60).stdout
+            _HIPCC_VERSION = " ".join(l.strip() for l in out.splitlines() if "version" in l.lower())
+        except (OSError, subprocess.SubprocessError):
+            _HIPCC_VERSION = "unknown"
+    return _HIPCC_VERSION
 
 
 def source_hash(root=ROOT):
-    """Hash of the kernel sources and build flags: identifies the build a record was measured on."""
+    """Hash of the library's sources, build flags and compiler version: identifies the build a
+    record was measured on. The Makefile embeds the same hash in the library (jt_version)."""
     import hashlib
     h = hashlib.sha256()
-    for f in BUILD_FILES:
+    for f in build_files(root):
         h.update(f.encode())
         h.update((root / f).read_bytes())
+    h.update(hipcc_version().encode())
     return h.hexdigest()[:16]
+
+
 CUS = 256
 XCDS = 8
 KERNEL_RE = re.compile(r"(trace_kernel\w*<\d+, \d+, (?:true|false), 0, \d+>)")
@@ -174,5 +197,9 @@ if __name__ == "__main__":
     m.add_argument("--out", required=True)
     c = sub.add_parser("check")
     c.add_argument("paths", nargs="+")
+    sub.add_parser("hash")
     a = ap.parse_args()
-    make(a) if a.cmd == "make" else check(a.paths)
+    if a.cmd == "hash":
+        print(source_hash())
+    else:
+        make(a) if a.cmd == "make" else check(a.paths)

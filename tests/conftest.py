@@ -31,6 +31,16 @@ def lib(abi):
     return abi.load_library()
 
 
+@pytest.fixture
+def options(abi, lib):
+    """Setter of the library's run-time options (jt_set_option) for contexts the test creates;
+    every option is removed again when the test ends."""
+    def set_(name, value):
+        abi.set_option(lib, name, value)
+    yield set_
+    abi.set_option(lib, None, None)
+
+
 @pytest.fixture(scope="session")
 def oracle(abi):
     from oracle import Oracle

@@ -33,8 +33,46 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_version(lib):
-    assert lib.jt_abi_version() == 2  # 2: jt_params.traversal
+    assert lib.jt_abi_version() == 3  # 2: jt_params.traversal, 3: jt_set_option
     assert b"gfx950" in lib.jt_version()
+
+
+def _check_build_matches_source(lib):
+    import sys
+    sys.path.insert(0, str(ROOT / "scripts"))
+    from roofline import source_hash
+    m = re.search(r"source ([0-9a-f]{16}|unknown)\)", lib.jt_version().decode())
+    assert m, lib.jt_version()
+    assert m.group(1) == source_hash(), (f"the loaded library was built from other sources ({m.group(1)}) than "
+                                         f"this tree ({source_hash()}): rebuild with make -C julia-raytracer_amd")
+
+
+def test_library_built_from_this_source(lib):
+    """jt_version() carries the source hash the Makefile embedded (every csrc/ file, the Makefile,
+    the ABI header, the hipcc version): the loaded binary was built from these sources."""
+    _check_build_matches_source(lib)
+
+
+@pytest.mark.gpu
+def test_gpu_box_library_built_from_this_source(gpu, lib):
+    """The same check where the GPU tests run: the prebuilt library that travelled to the box
+    was built from the committed sources, not from an older tree."""
+    _check_build_matches_source(lib)
+
+
+def test_run_time_options_are_explicit(abi, lib):
+    """Run-time options come only from jt_set_option: unknown names are rejected, known ones set
+    and clear, and the library never reads the environment (no getenv in the sources)."""
+    assert lib.jt_set_option(b"no_such_option", b"1") == -1
+    assert b"unknown option" in lib.jt_last_error()
+    for name in ("env_alias", "features", "lds_scene", "lds_stack", "light_inline", "chunk", "chunk_min",
+                 "wait_lanes", "light_lanes", "multi_split", "test_tiles", "test_lds_ring"):
+        assert lib.jt_set_option(name.encode(), b"1") == 0
+        assert lib.jt_set_option(name.encode(), None) == 0
+    assert lib.jt_set_option(None, b"1") == -1
+    assert lib.jt_set_option(None, None) == 0
+    for src in (ROOT / "julia-raytracer_amd" / "csrc").glob("*"):
+        assert "getenv" not in src.read_text(), src
 
 
 STRUCTS = ["jt_camera", "jt_instance", "jt_environment", "jt_material", "jt_texture", "jt_shape", "jt_scene",

@@ -1,4 +1,4 @@
-"""Environment-light alias tables (JT_ENV_ALIAS=1; SURVEY §8(f) rank 3, src/trace.jl:968-1008 and
+"""Environment-light alias tables (option env_alias=1; SURVEY §8(f) rank 3, src/trace.jl:968-1008 and
 src/sampling.jl:33-56): an O(1) Vose alias draw replaces upper_bound over the environment CDF.
 It samples the same pmf but maps random numbers to texels differently, so it cannot be
 bit-exact with the reference's upper_bound: it is a non-default statistical variant. Checked
@@ -16,12 +16,12 @@ from test_gpu_scenes import scene_abi
 pytestmark = pytest.mark.gpu
 
 
-def _render(abi, lib, sa, p, spp, alias, monkeypatch):
+def _render(abi, lib, sa, p, spp, alias, options):
     from jtrace import trace
     if alias:
-        monkeypatch.setenv("JT_ENV_ALIAS", "1")
+        options("env_alias", "1")
     else:
-        monkeypatch.delenv("JT_ENV_ALIAS", raising=False)
+        options("env_alias", None)
     bvh = trace.make_scene_bvh(sa, False, lib)
     lights = trace.make_trace_lights(sa, lib)
     st = trace.make_trace_state(sa, bvh, lights, p, lib)
@@ -32,18 +32,18 @@ def _render(abi, lib, sa, p, spp, alias, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["features1", "features2"])
-def test_alias_pin_reference_render(gpu, abi, lib, monkeypatch, name):
-    monkeypatch.setenv("JT_ENV_ALIAS", "1")
+def test_alias_pin_reference_render(gpu, abi, lib, options, name):
+    options("env_alias", "1")
     tgs.test_statistical_pin_reference_render(gpu, abi, lib, name, 1)
 
 
 @pytest.mark.parametrize("name", ["features1", "ecosys"])
-def test_alias_matches_default_path_statistically(gpu, abi, lib, monkeypatch, name):
+def test_alias_matches_default_path_statistically(gpu, abi, lib, options, name):
     sa = scene_abi(name)
     spp = 64
     p = make_params(abi, resolution=128, samples=spp, batch=spp)
-    ref = _render(abi, lib, sa, p, spp, False, monkeypatch)
-    ali = _render(abi, lib, sa, p, spp, True, monkeypatch)
+    ref = _render(abi, lib, sa, p, spp, False, options)
+    ali = _render(abi, lib, sa, p, spp, True, options)
     assert "env_alias=0" in ref[2] and "env_alias=1" in ali[2], (ref[2], ali[2])
     assert not np.array_equal(ref[0], ali[0])
     cm_r = ref[0][..., :3].reshape(-1, 3).mean(axis=0)

@@ -10,6 +10,11 @@ its own test so that no single test runs for more than about half a minute. Bar 
 tests/test_gpu_parity.py: >= 99.9 % of pixels within 1e-3 relative on every channel, the band's
 image mean within 1e-4 relative, hit counts identical; over the whole frame, the closest-hit ray
 and light-query counts within 0.1 % + 8.
+
+Every frame is checked in both BVH child orders: near-first (DEFAULT_TRAVERSAL, the order bench.py
+times) and the reference's far-first order (src/bvh.jl:331-341); the oracle restates both. The
+fraction of pixels whose near-order value differs from the reference-order value at all (exact-t
+ties only) is printed per frame.
 """
 import numpy as np
 import pytest
@@ -21,31 +26,37 @@ pytestmark = pytest.mark.gpu
 
 # scene: (width, height, row bands)
 FRAMES = {"features2": (1920, 1080, 1), "bathroom1": (1920, 1080, 2), "ecosys": (3840, 1920, 4)}
+ORDERS = ["near", "reference"]
 _gpu = {}
 _oracle_counts = {}
 
 
-def gpu_frame(lib, abi, name):
-    if name not in _gpu:
+def gpu_frame(lib, abi, name, order):
+    if (name, order) not in _gpu:
         from jtrace import trace
         W, H, _ = FRAMES[name]
         sa = scene_abi(name)
-        p = make_params(abi, resolution=W, samples=1, width=W, height=H)
+        p = make_params(abi, resolution=W, samples=1, width=W, height=H, traversal=order)
         st = trace.make_trace_state(sa, trace.make_scene_bvh(sa, False, lib), trace.make_trace_lights(sa, lib), p, lib)
         st.set_counters(1)
         st.trace_range(0, 1)
-        _gpu[name] = (p, st.get_image(), *st.get_aovs(), st.counters(), st.describe())
+        _gpu[(name, order)] = (p, st.get_image(), *st.get_aovs(), st.counters(), st.describe())
         st.close()
-    return _gpu[name]
+        other = [k for k in _gpu if k[0] == name and k[1] != order]
+        if other:
+            a, b = _gpu[(name, "near")][1], _gpu[(name, "reference")][1]
+            print(f"{name} {W}x{H}x1: pixels differing between the near and reference orders "
+                  f"{float(np.mean(np.any(a != b, axis=-1))):.3e}")
+    return _gpu[(name, order)]
 
 
-CASES = [(n, b) for n, (_, _, nb) in FRAMES.items() for b in range(nb)]
+CASES = [(n, o, b) for o in ORDERS for n, (_, _, nb) in FRAMES.items() for b in range(nb)]
 
 
-@pytest.mark.parametrize("name,band", CASES, ids=[f"{n}-band{b}" for n, b in CASES])
-def test_full_frame_band_parity(gpu, abi, lib, oracle, name, band):
+@pytest.mark.parametrize("name,order,band", CASES, ids=[f"{n}-{o}-band{b}" for n, o, b in CASES])
+def test_full_frame_band_parity(gpu, abi, lib, oracle, name, order, band):
     W, H, nb = FRAMES[name]
-    p, img, alb, nrm, hits, cnt, desc = gpu_frame(lib, abi, name)
+    p, img, alb, nrm, hits, cnt, desc = gpu_frame(lib, abi, name, order)
     assert img.shape == (H, W, 4)
     r0, r1 = band * H // nb, (band + 1) * H // nb
     sa = scene_abi(name)
@@ -54,19 +65,19 @@ def test_full_frame_band_parity(gpu, abi, lib, oracle, name, band):
     g = (img[r0:r1], alb[r0:r1], nrm[r0:r1], hits[r0:r1])
     o = (oimg[r0:r1], oalb[r0:r1], onrm[r0:r1], ohits[r0:r1])
     stats = compare_images(g[0], o[0])
-    print(f"{name} rows [{r0}, {r1}) {desc.split()[0]}: {stats}")
+    print(f"{name} traversal={order} rows [{r0}, {r1}) {desc.split()[0]}: {stats}")
     assert stats["frac_pix_rel_le_1e-3"] >= 0.999, stats
     assert stats["image_mean_rel"] <= 1e-4, stats
     assert np.array_equal(g[3], o[3])
     for a, b in ((g[1], o[1]), (g[2], o[2])):
         s = compare_images(a, b)
         assert s["frac_pix_rel_le_1e-3"] >= 0.999, s
-    acc = _oracle_counts.setdefault(name, {})
+    acc = _oracle_counts.setdefault((name, order), {})
     for k in ("rays", "light_queries", "paths"):
         acc[k] = acc.get(k, 0) + ocnt[k]
     acc["bands"] = acc.get("bands", 0) + 1
     if acc["bands"] == nb:  # the whole frame checked: its ray counts too
-        print(f"{name} frame counts: gpu {cnt}, oracle {acc}")
+        print(f"{name} traversal={order} frame counts: gpu {cnt}, oracle {acc}")
         assert cnt["paths"] == acc["paths"] == W * H
         for k in ("rays", "light_queries"):
             assert abs(cnt[k] - acc[k]) <= 1e-3 * acc[k] + 8, (k, cnt[k], acc[k])

@@ -123,7 +123,7 @@ def test_statistical_pin_full_resolution(gpu, abi, lib, cornell_abi):
 
 
 @pytest.mark.parametrize("sampler", [1, 2])
-def test_lds_and_hbm_scene_modes_bitwise_equal(gpu, abi, lib, cornell_abi, sampler, monkeypatch):
+def test_lds_and_hbm_scene_modes_bitwise_equal(gpu, abi, lib, cornell_abi, sampler, options):
     """The small-scene LDS mode and the HBM mode run the same program on the same data."""
     from jtrace import trace
     bvh = trace.make_scene_bvh(cornell_abi, False, lib)
@@ -131,7 +131,7 @@ def test_lds_and_hbm_scene_modes_bitwise_equal(gpu, abi, lib, cornell_abi, sampl
     p = make_params(abi, resolution=80, samples=4, sampler=sampler)
     imgs = []
     for mode in ("0", "65536"):
-        monkeypatch.setenv("JT_LDS_SCENE", mode)
+        options("lds_scene", mode)
         st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
         st.trace_range(0, 4)
         imgs.append((st.get_image(), st.get_aovs(), st.counters()))
@@ -145,17 +145,17 @@ def test_lds_and_hbm_scene_modes_bitwise_equal(gpu, abi, lib, cornell_abi, sampl
 
 @pytest.mark.parametrize("sampler", [1, 2])
 @pytest.mark.parametrize("lds", ["65536", "0"])
-def test_feature_specialisation_bitwise_equal(gpu, abi, lib, cornell_abi, sampler, lds, monkeypatch):
+def test_feature_specialisation_bitwise_equal(gpu, abi, lib, cornell_abi, sampler, lds, options):
     """Cornellbox has no scene feature bit, so it runs the FT_NONE kernel; the general FT_ALL
-    kernel (JT_FEATURES=all) must give the same bits, counters included."""
+    kernel (option features=all) must give the same bits, counters included."""
     from jtrace import trace
     bvh = trace.make_scene_bvh(cornell_abi, False, lib)
     lights = trace.make_trace_lights(cornell_abi, lib)
     p = make_params(abi, resolution=80, samples=4, sampler=sampler)
-    monkeypatch.setenv("JT_LDS_SCENE", lds)
+    options("lds_scene", lds)
     outs = []
     for feat in ("auto", "all"):
-        monkeypatch.setenv("JT_FEATURES", feat)
+        options("features", feat)
         st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
         st.set_counters(1)
         st.trace_range(0, 4)
@@ -169,7 +169,7 @@ def test_feature_specialisation_bitwise_equal(gpu, abi, lib, cornell_abi, sample
         assert outs[0][2][k] == outs[1][2][k], k
 
 
-def test_light_hit_steps_are_bitwise_invariant(gpu, abi, lib, cornell_abi, monkeypatch):
+def test_light_hit_steps_are_bitwise_invariant(gpu, abi, lib, cornell_abi, options):
     """Light-hit steps inside the traversal phase (FT_NONE kernel, path sampler) only change
     when a lane runs light_hit, not what it computes: every threshold gives the same bits."""
     from jtrace import trace
@@ -177,9 +177,9 @@ def test_light_hit_steps_are_bitwise_invariant(gpu, abi, lib, cornell_abi, monke
     lights = trace.make_trace_lights(cornell_abi, lib)
     p = make_params(abi, resolution=72, samples=5, sampler=1)
     outs = []
-    monkeypatch.setenv("JT_LIGHT_INLINE", "0")  # cornellbox's light chains otherwise never leave the shading phase
+    options("light_inline", "0")  # cornellbox's light chains otherwise never leave the shading phase
     for ll in ("1", "7", "65"):
-        monkeypatch.setenv("JT_LIGHT_LANES", ll)
+        options("light_lanes", ll)
         st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
         st.set_counters(1)
         st.trace_range(0, 5)
@@ -194,7 +194,7 @@ def test_light_hit_steps_are_bitwise_invariant(gpu, abi, lib, cornell_abi, monke
 
 
 @pytest.mark.parametrize("sampler", [1, 2])
-def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sampler, monkeypatch):
+def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sampler, options):
     """Work units = (sample chunk, 8x8 tile), fetched dynamically by waves: a tile's chunks are
     accumulated in order (cross-XCD release/acquire), so any chunk size gives the same bits."""
     from jtrace import trace
@@ -202,14 +202,14 @@ def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sa
     lights = trace.make_trace_lights(cornell_abi, lib)
     p = make_params(abi, resolution=72, samples=9, sampler=sampler)
     outs = []
-    # uniform chunks of 1000 (one per tile), 1 and 4 samples (JT_CHUNK_MIN=0); chunk tables
+    # uniform chunks of 1000 (one per tile), 1 and 4 samples (option chunk_min=0); chunk tables
     # ending in a halving tail: 4,3,1,1 and 2,2,2,2,1; the auto tail of 64-sample chunks (9 samples: one chunk)
     for chunk, cmin in (("1000", "0"), ("1", "0"), ("4", "0"), ("4", "1"), ("2", "1"), ("64", None)):
-        monkeypatch.setenv("JT_CHUNK", chunk)
+        options("chunk", chunk)
         if cmin is None:
-            monkeypatch.delenv("JT_CHUNK_MIN", raising=False)
+            options("chunk_min", None)
         else:
-            monkeypatch.setenv("JT_CHUNK_MIN", cmin)
+            options("chunk_min", cmin)
         st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
         st.trace_range(0, 9)
         outs.append((st.get_image(), st.get_aovs(), st.counters()))
@@ -278,15 +278,23 @@ def _full_parity(abi, lib, oracle, scene_abi, params, spp, label):
         assert compare_images(a, b)["frac_pix_rel_le_1e-3"] >= 0.999
 
 
-def test_headline_frame_parity(gpu, abi, lib, oracle, cornell_abi):
+# "near" is the order bench.py times (DEFAULT_TRAVERSAL); "reference" is the reference's own
+# far-first order (src/bvh.jl:331-341). Both are restated by the oracle.
+ORDERS = ["near", "reference"]
+
+
+@pytest.mark.parametrize("order", ORDERS)
+def test_headline_frame_parity(gpu, abi, lib, oracle, cornell_abi, order):
     """The bench's exact framing — cornellbox path at 1280x720 through --width/--height, whose
     film is fitted to W/H (the oracle restates that override) — against the oracle, full frame,
-    8 spp (the headline workload's first 8 samples of every pixel)."""
-    params = make_params(abi, width=1280, height=720, samples=8, sampler=1)
-    _full_parity(abi, lib, oracle, cornell_abi, params, 8, "cornellbox path 1280x720x8")
+    8 spp (the headline workload's first 8 samples of every pixel), in the benched near-first
+    order and in the reference's order."""
+    params = make_params(abi, width=1280, height=720, samples=8, sampler=1, traversal=order)
+    _full_parity(abi, lib, oracle, cornell_abi, params, 8, f"cornellbox path 1280x720x8 traversal={order}")
 
 
-def test_config1_full_size_parity(gpu, abi, lib, oracle, cornell_abi):
+@pytest.mark.parametrize("order", ORDERS)
+def test_config1_full_size_parity(gpu, abi, lib, oracle, cornell_abi, order):
     """BASELINE config 1 at its own size: cornellbox naive 256x256 x 16 spp (1,048,576 paths)."""
-    params = make_params(abi, resolution=256, samples=16, sampler=2)
-    _full_parity(abi, lib, oracle, cornell_abi, params, 16, "config1 cornellbox naive 256x256x16")
+    params = make_params(abi, resolution=256, samples=16, sampler=2, traversal=order)
+    _full_parity(abi, lib, oracle, cornell_abi, params, 16, f"config1 cornellbox naive 256x256x16 traversal={order}")

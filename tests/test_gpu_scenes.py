@@ -141,9 +141,9 @@ def test_statistical_pin_reference_render(gpu, abi, lib, name, sampler):
 
 
 @pytest.mark.parametrize("name,ring", [("cornellbox", 1), ("shapes1", 2), ("bathroom1", 4)])
-def test_stack_overflow_to_hbm_is_exact(gpu, abi, lib, monkeypatch, name, ring):
+def test_stack_overflow_to_hbm_is_exact(gpu, abi, lib, options, name, ring):
     """The LDS stack ring spills its oldest entries to HBM and reloads them when popped: with a
-    deliberately tiny ring (JT_LDS_RING, test-only) every deep traversal overflows, and the
+    deliberately tiny ring (option test_lds_ring, test-only) every deep traversal overflows, and the
     image, AOVs and traversal counters must not change at all."""
     from jtrace import sceneio, trace
     sa = abi.SceneABI(sceneio.load_scene(CORNELL)) if name == "cornellbox" else scene_abi(name)
@@ -153,9 +153,9 @@ def test_stack_overflow_to_hbm_is_exact(gpu, abi, lib, monkeypatch, name, ring):
     outs = []
     for env in (None, str(ring)):
         if env is None:
-            monkeypatch.delenv("JT_LDS_RING", raising=False)
+            options("test_lds_ring", None)
         else:
-            monkeypatch.setenv("JT_LDS_RING", env)
+            options("test_lds_ring", env)
         st = trace.make_trace_state(sa, bvh, lights, p, lib)
         st.trace_range(0, 3)
         outs.append((st.get_image(), st.get_aovs(), st.counters(), st.describe()))
@@ -169,11 +169,11 @@ def test_stack_overflow_to_hbm_is_exact(gpu, abi, lib, monkeypatch, name, ring):
 
 
 @pytest.mark.parametrize("name,mask", [("bathroom1", ",8363> "), ("ecosys", ",16571> "), ("features2", ",8383> ")])
-def test_mesh_specialisations_bitwise_equal(gpu, abi, lib, monkeypatch, name, mask):
+def test_mesh_specialisations_bitwise_equal(gpu, abi, lib, options, name, mask):
     """Configs 3-5 run the large-scene specialisations (FT_MESH, FT_MESH_ENV, FT_MESH_ENV_QUAD,
     HBM mode with the child pre-test; features2 with light-hit steps that defer environment pdf
     terms to the shading phase): the general FT_ALL kernel
-    (JT_FEATURES=all) must give the same image, AOVs and traversal counters, bit for bit."""
+    (option features=all) must give the same image, AOVs and traversal counters, bit for bit."""
     from jtrace import trace
     sa = scene_abi(name)
     p = make_params(abi, resolution=96, samples=2)
@@ -181,7 +181,7 @@ def test_mesh_specialisations_bitwise_equal(gpu, abi, lib, monkeypatch, name, ma
     lights = trace.make_trace_lights(sa, lib)
     outs = []
     for feat in ("auto", "all"):
-        monkeypatch.setenv("JT_FEATURES", feat)
+        options("features", feat)
         st = trace.make_trace_state(sa, bvh, lights, p, lib)
         st.set_counters(1)
         st.trace_range(0, 2)
@@ -197,22 +197,22 @@ def test_mesh_specialisations_bitwise_equal(gpu, abi, lib, monkeypatch, name, ma
 
 @pytest.mark.parametrize("name,lds", [("cornellbox", "65536"), ("cornellbox", "0"), ("bathroom1", None),
                                       ("features2", None), ("materials1", None)])
-def test_inline_light_chains_bitwise_equal(gpu, abi, lib, monkeypatch, name, lds):
+def test_inline_light_chains_bitwise_equal(gpu, abi, lib, options, name, lds):
     """Scenes whose instance lights are one-leaf shape BVHs run sample_lights_pdf's light chain
     inline in the shading phase (DScene::light_inline) instead of through the traversal loop and
     its light-hit steps. The same node/primitive steps in the same per-lane order: images, AOVs
-    and every counter must be bit-identical to the traversal path (JT_LIGHT_INLINE=0), in the
+    and every counter must be bit-identical to the traversal path (option light_inline=0), in the
     LDS-mode FT_NONE kernel (cornellbox), its HBM mode, and the mesh kernels."""
     from jtrace import sceneio, trace
     sa = abi.SceneABI(sceneio.load_scene(CORNELL)) if name == "cornellbox" else scene_abi(name)
     if lds is not None:
-        monkeypatch.setenv("JT_LDS_SCENE", lds)
+        options("lds_scene", lds)
     p = make_params(abi, resolution=96, samples=3)
     bvh = trace.make_scene_bvh(sa, False, lib)
     lights = trace.make_trace_lights(sa, lib)
     outs = []
     for inl in ("1", "0"):
-        monkeypatch.setenv("JT_LIGHT_INLINE", inl)
+        options("light_inline", inl)
         st = trace.make_trace_state(sa, bvh, lights, p, lib)
         st.set_counters(1)
         st.trace_range(0, 3)

@@ -18,18 +18,34 @@ from test_gpu_scenes import check_parity, render_gpu, render_oracle, scene_abi
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("order", ["near", "reference"])
 @pytest.mark.parametrize("sampler", [1, 2])
 @pytest.mark.parametrize("name,lds", [("cornellbox", "lds"), ("cornellbox", "hbm"), ("features1", None),
                                       ("features2", None), ("bathroom1", None), ("ecosys", None)])
-def test_near_order_parity(gpu, abi, lib, oracle, cornell_abi, name, lds, sampler, monkeypatch):
-    """HIP vs oracle, both in near-first order (LDS and HBM scene modes for cornellbox)."""
+def test_order_parity(gpu, abi, lib, oracle, cornell_abi, name, lds, sampler, order, options):
+    """HIP vs oracle in each child order (LDS and HBM scene modes for cornellbox)."""
     if lds == "hbm":
-        monkeypatch.setenv("JT_LDS_SCENE", "0")
+        options("lds_scene", "0")
     sa = cornell_abi if name == "cornellbox" else scene_abi(name)
-    p = make_params(abi, resolution=120, samples=4, sampler=sampler, traversal="near")
+    p = make_params(abi, resolution=120, samples=4, sampler=sampler, traversal=order)
     g = render_gpu(lib, sa, p, 0, 4)
     o = render_oracle(oracle, sa, p, g[0].shape[1], g[0].shape[0], 0, 4)
-    check_parity(g, o, f"{name}/{lds}/{sampler}/near")
+    check_parity(g, o, f"{name}/{lds}/{sampler}/{order}")
+
+
+def test_abi_zero_value_is_reference_order(gpu, abi, lib, oracle, cornell_abi):
+    """A C caller that zero-fills jt_params (traversal = 0, JT_TRAVERSAL_REFERENCE) gets the
+    reference's far-first order: its image equals the explicit reference-order render bit for bit
+    and meets the parity bar against the oracle's reference order."""
+    p0 = make_params(abi, resolution=96, samples=4)
+    p0.traversal = 0  # the C-ABI zero value
+    ref = make_params(abi, resolution=96, samples=4, traversal="reference")
+    assert ref.traversal == 0
+    g = render_gpu(lib, cornell_abi, p0, 0, 4)
+    r = render_gpu(lib, cornell_abi, ref, 0, 4)
+    assert np.array_equal(g[0], r[0]) and g[4]["nodes"] == r[4]["nodes"]
+    o = render_oracle(oracle, cornell_abi, ref, g[0].shape[1], g[0].shape[0], 0, 4)
+    check_parity(g, o, "cornellbox/zero-value/reference")
 
 
 @pytest.mark.parametrize("name", ["cornellbox", "features2", "bathroom1", "ecosys"])

@@ -21,6 +21,12 @@ def test_oracle_near_order_matches_reference_order(abi, oracle, cornell_abi):
 
 
 def test_params_carry_the_traversal_order(abi):
-    assert make_params(abi).traversal == 0
+    from jtrace.cli import DEFAULT_TRAVERSAL, Params, parse_cli_args
+    # one default for the parser, the dataclass and make_params: near first (the benched order)
+    assert DEFAULT_TRAVERSAL == "near"
+    assert Params(scene="x").traversal == parse_cli_args(["--scene", "x"]).traversal == DEFAULT_TRAVERSAL
+    assert make_params(abi).traversal == 1
     assert make_params(abi, traversal="near").traversal == 1
+    assert make_params(abi, traversal="reference").traversal == 0
+    assert abi.jt_params().traversal == 0  # the C-ABI zero value is the reference's order
     assert abi.jt_params.traversal.offset == 64 and abi.C.sizeof(abi.jt_params) == 72
