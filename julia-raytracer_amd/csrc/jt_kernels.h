@@ -691,8 +691,14 @@ constexpr unsigned CTL_BOUNCE = 0x7fffu, CTL_OPB = 15, CTL_FLAGS = 23, CTL_LC = 
 #ifndef JT_PARK
 #define JT_PARK 1
 #endif
-constexpr int PARK_SLOTS = 7;  // radiance xyz, max_roughness, lq xyz
-// slots: [0, 3) radiance, 3 max_roughness, [4, 7) lq. The mesh kernels park (features2 +6 %,
+// pb (sample_bsdfcos_pdf of the bounce) is read once, after the bounce's whole light chain: in
+// the FT_LINL mesh kernels the chain runs inline, and a register kept live across it was spilled
+// and written back to scratch every shading phase (features2: 9.1 GB of WRITE per launch)
+#ifndef JT_PARK_PB
+#define JT_PARK_PB 1
+#endif
+constexpr int PARK_SLOTS = 7 + (JT_PARK_PB ? 1 : 0);  // radiance xyz, max_roughness, lq xyz, pb
+// slots: [0, 3) radiance, 3 max_roughness, [4, 7) lq, 7 pb. The mesh kernels park (features2 +6 %,
 // bathroom1 +14 %, ecosys +9 %: their spills fell from 12-28 to 0-7 VGPRs). The FT_NONE kernel
 // (cornellbox, 2-8 spilled VGPRs either way) does not: its light-hit steps read the light-chain
 // position every few traversal iterations, and parking cost 4-11 % there (profiles/r03_park/).
@@ -742,6 +748,13 @@ struct Path {
         if (park(F)) pk[3 * BLOCK] = v;
         else max_roughness_ = v;
     }
+    template <int F>
+    __device__ __forceinline__ float pb() const { return park(F) && JT_PARK_PB ? pk[7 * BLOCK] : pb_; }
+    template <int F>
+    __device__ __forceinline__ void set_pb(float v) {
+        if (park(F) && JT_PARK_PB) pk[7 * BLOCK] = v;
+        else pb_ = v;
+    }
     __device__ __forceinline__ int bounce() const { return (int)(ctl & CTL_BOUNCE); }
     __device__ __forceinline__ int opbounce() const { return (int)((ctl >> CTL_OPB) & 0xffu); }
     __device__ __forceinline__ bool flag(int f) const { return (ctl >> CTL_FLAGS) & (unsigned)f; }
@@ -750,7 +763,7 @@ struct Path {
     __device__ __forceinline__ int lcount() const { return (int)(ctl >> CTL_LC); }
     v3 lq_;      // during PH_LIGHT: the shading position (st.o holds the light query's origin,
                  // next_position of src/trace.jl:1039, so every query's ray is (st.o, st.d))
-    float pb;    // sample_bsdfcos_pdf / sample_scattering_pdf
+    float pb_;   // sample_bsdfcos_pdf / sample_scattering_pdf (pb<F>(): parked in the mesh kernels)
     float pdf, lpdf;
     Volume vol;  // volume_stack[1] (the stack never holds more than one entry)
 };
@@ -788,7 +801,7 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
         if (st.li >= S.nlights) {
             st.o = st.lq<F>();  // the next bounce's ray starts at the shading position
             const float pdf = st.pdf * S.light_pick_pdf;  // sample_uniform_pdf(nlights), host-computed
-            st.weight = st.weight / (0.5f * st.pb + 0.5f * pdf);  // (weight .* f) / (...)
+            st.weight = st.weight / (0.5f * st.pb<F>() + 0.5f * pdf);  // (weight .* f) / (...)
             return after_weight(P, st);
         }
         const DLight l = S.lights[st.li];
@@ -966,7 +979,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
             }
             if (is_zero(incoming)) return true;
             st.weight = st.weight * eval_bsdfcos<F>(sh.mat, sh.normal, outgoing, incoming);
-            st.pb = sample_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
+            st.set_pb<F>(sample_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming));
         } else {
             float rnl = rand1f(st.rng);
             incoming = sample_delta<F>(sh.mat, sh.normal, outgoing, rnl);
@@ -1006,7 +1019,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
     }
     if (is_zero(incoming)) return true;
     st.weight = st.weight * eval_scattering(st.vol, outgoing, incoming);
-    st.pb = sample_scattering_pdf(st.vol, outgoing, incoming);
+    st.set_pb<F>(sample_scattering_pdf(st.vol, outgoing, incoming));
     st.o = position;
     st.d = incoming;
     return begin_light_pdf<F>(S, P, st);
