@@ -27,6 +27,7 @@ from jtrace.cli import DEFAULT_TRAVERSAL  # noqa: E402  (pure Python: no torch, 
 
 METRIC_BASE = "Mrays/s + wall-clock render time"  # BASELINE.json metric; the workload is appended
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SIGNATURES = ROOT / "profiles" / "image_signatures.json"  # one-GPU image fingerprints per workload
 
 
 def metric_name(scene: str, sampler: str, W: int, H: int, S: int) -> str:
@@ -35,11 +36,11 @@ def metric_name(scene: str, sampler: str, W: int, H: int, S: int) -> str:
     return f"{METRIC_BASE}, {scene} {W}×{H}×{S}spp" + ("" if sampler == "path" else f" ({sampler} sampler)")
 
 
-def algorithmic_bytes(c: dict, shade_bytes: int, quad_scene: bool) -> int:
-    """Algorithmic bytes of the trace launches: 32 B per BVH node pop,
-    64 B per instance visit, 48 B per triangle test (64 B per quad test), shade_bytes per
-    surface hit."""
-    return (32 * c["nodes"] + 64 * c["instances"] + (64 if quad_scene else 48) * c["prims"]
+def algorithmic_bytes(c: dict, shade_bytes: int, quad_scene: bool, wide: bool = False) -> int:
+    """Algorithmic bytes of the trace launches: 32 B per BVH node pop (64 B
+    per wide-record visit, which tests up to four child boxes), 64 B per instance visit, 48 B per
+    triangle test (64 B per quad test), shade_bytes per surface hit."""
+    return ((64 if wide else 32) * c["nodes"] + 64 * c["instances"] + (64 if quad_scene else 48) * c["prims"]
             + shade_bytes * c["shades"])
 
 
@@ -104,7 +105,7 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--sampler", default="path")
     ap.add_argument("--scene", default=str(ROOT / "assets" / "scenes" / "cornellbox" / "cornellbox.json"))
-    ap.add_argument("--traversal", choices=["reference", "near"], default=DEFAULT_TRAVERSAL,
+    ap.add_argument("--traversal", choices=["reference", "near", "wide"], default=DEFAULT_TRAVERSAL,
                     help="BVH child order (include/jtrace.h jt_traversal): near child first (the default, the "
                          "product's order) or the reference's far-first order (src/bvh.jl:331-341)")
     ap.add_argument("--no-reference-order", action="store_true",
@@ -114,6 +115,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-spp", type=int, default=128)
+    ap.add_argument("--write-signature", action="store_true",
+                    help="N=1: record this workload's image fingerprint in profiles/image_signatures.json")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="a library run-time option (jt_set_option, include/jtrace.h) for A/B runs; repeatable")
     args = ap.parse_args()
@@ -163,7 +166,8 @@ def main():
             "lights_s": round(t_lights - t_bvh, 3), "upload_s": round(t_create - t_lights, 3),
             "total_s": round(t_create - t_0, 3)}
     W, H, S = state.width, state.height, args.spp
-    from jtrace.parallel import reduce_running_means, shard_range
+    from jtrace.parallel import (compare_signature, image_signature, load_signature, reduce_running_means,
+                                 save_signature, shard_range)
     s0, s1 = shard_range(S, world, rank)
 
     img_t = None
@@ -175,11 +179,13 @@ def main():
                                         "data": (buf.image, False), "version": 3}
         img_t = torch.as_tensor(_CAI(), device=f"cuda:{dev}")
 
+    reduced = [None]  # rank 0, N > 1: the last step's reduced image (the image check below)
+
     def step():
         state.reset()
         state.trace_range(s0, s1)  # returns when the launch has finished (HIP event sync)
         if world > 1:  # the path's one exchange: sum of sample-weighted shard means (RCCL)
-            reduce_running_means(img_t if backend == "nccl" else img_t.cpu(), s1 - s0, S, dist, dst=0)
+            reduced[0] = reduce_running_means(img_t if backend == "nccl" else img_t.cpu(), s1 - s0, S, dist, dst=0)
             # the reduce reads the library's buffer on torch's stream: finish it before the next
             # step's jt_reset clears that buffer on the library's stream
             torch.cuda.synchronize()
@@ -222,6 +228,26 @@ def main():
         elapsed, total_rays = float(tmax[0]), float(t[1])
     else:
         total_rays = float(rays)
+
+    # Image check (rank 0, every N): block means of the final image — the RCCL-reduced one for
+    # N > 1 — against the one-GPU signature committed for this workload (profiles/image_signatures.json,
+    # jtrace/parallel.py): a wrong shard split, weight or reduce fails the run loudly
+    image_check = None
+    if rank == 0:
+        img_final = (reduced[0].detach().cpu().numpy().reshape(H, W, 4) if world > 1 else state.get_image())
+        sig = image_signature(img_final)
+        sig_key = f"{Path(args.scene).stem} {args.sampler} {W}x{H}x{S}spp traversal={args.traversal}" + \
+            (" bvh=sah" if args.highqualitybvh else "")
+        ref_sig = load_signature(SIGNATURES, sig_key)
+        if args.write_signature and world == 1:
+            save_signature(SIGNATURES, sig_key, sig, "one-GPU bench.py run, block means of the final image")
+            image_check = {"key": sig_key, "written": str(SIGNATURES.relative_to(ROOT))}
+        elif ref_sig is not None:
+            image_check = {"key": sig_key, **compare_signature(sig, ref_sig), "ranks_reduced": world}
+            if not image_check["ok"]:
+                raise SystemExit(f"image check failed for {sig_key}: {image_check}")
+        else:
+            image_check = {"key": sig_key, "ok": None, "why": "no committed signature for this workload"}
 
     # Reference-order leg (rank 0, N=1): the same workload with the reference's far-child-first
     # order (src/bvh.jl:331-341, SURVEY Appendix B item 9: performance only), timed the same way,
@@ -283,7 +309,7 @@ def main():
         avg_launch_s = kernel_ms / launches / 1e3
         per_launch = {k: v / max(1, full["launches"]) for k, v in full.items()}  # one step's launches
         logical = algorithmic_bytes(per_launch, shade_record_bytes(scene),
-                                    any(len(s.quads) for s in scene.shapes))
+                                    any(len(s.quads) for s in scene.shapes), args.traversal == "wide")
         workload = f"{name} {args.sampler} {W}x{H} {s1 - s0} samples/launch" + \
             ("" if args.traversal == "reference" else f" traversal={args.traversal}") + \
             (" bvh=sah" if args.highqualitybvh else "")
@@ -352,6 +378,7 @@ def main():
             "options": dict(o.partition("=")[::2] for o in args.opt) or None,
             "roofline": roof,
             "reference_order": ref_order,
+            "image_check": image_check,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

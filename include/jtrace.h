@@ -78,8 +78,17 @@ typedef enum jt_sampler { JT_SAMPLER_PATH = 1, JT_SAMPLER_NAIVE = 2 } jt_sampler
  * JT_TRAVERSAL_NEAR: the opposite push order, the near child by the split axis first. The closest
  *   hit is the same up to ties: among hits at exactly equal t the later-tested wins
  *   (src/geometry.jl:226, t > tmax rejects), so only exact-t ties (and a box culled by the slab
- *   test's rounding) can resolve differently. Fewer nodes are visited (tmax shrinks sooner). */
-typedef enum jt_traversal { JT_TRAVERSAL_REFERENCE = 0, JT_TRAVERSAL_NEAR = 1 } jt_traversal;
+ *   test's rounding) can resolve differently. Fewer nodes are visited (tmax shrinks sooner).
+ * JT_TRAVERSAL_WIDE: the reference's binary tree collapsed to 4-wide records (each internal node
+ *   holds its grandchildren: same leaves, same primitive order) with conservative 8-bit quantised
+ *   child boxes, visited near child first in the binary DFS order. A box can only pass where the
+ *   exact one would, or more often, so again only exact-t ties and boxes the exact slab test culls
+ *   by rounding can resolve differently; one 64-B record replaces about three 32-B node visits. */
+typedef enum jt_traversal {
+    JT_TRAVERSAL_REFERENCE = 0,
+    JT_TRAVERSAL_NEAR = 1,
+    JT_TRAVERSAL_WIDE = 2
+} jt_traversal;
 
 /* CameraData (src/scene.jl:48-86), after the lookat conversion done by the loader. */
 typedef struct jt_camera {

@@ -30,6 +30,26 @@ namespace jtd {
 struct alignas(16) DNode {
     float4 a, b;
 };
+// Wide (4-ary) node record, 64 B = four 16-B loads: the traversal jt_params.traversal =
+// JT_TRAVERSAL_WIDE. A record stands for an internal binary node N of the
+// reference's tree (or a leaf root) and holds N's grandchildren: N's two children, each internal
+// child replaced by its own two children, so one visit tests up to four boxes and a DFS visits the
+// reference's leaves in the binary order. The boxes are conservative 8-bit quantisations relative
+// to N's box (dequantised lo = origin + q * scale in float, never above the exact bmin; hi never
+// below bmax), tested with the reference's intersect_bbox:
+//   r0: origin.xyz = N's bmin, meta bits = ex | ey << 8 | ez << 16 | (a0 | a1 << 2 | a2 << 4) << 24
+//       (scale of an axis = the float with biased exponent e, 2^(e - 127); a0 = N's split axis,
+//       a1 / a2 the split axes of N's children L / R, 0 for a leaf child)
+//   r1: bytes lo.x[4] hi.x[4] lo.y[4] hi.y[4] of slots 0..3; r2: lo.z[4] hi.z[4], 0, 0
+//   r3: child words of slots [LL, LR, RL, RR] (a leaf child L / R takes slot 0 / 2 alone)
+// child word: W_EMPTY; bit 31 clear: a record index; bit 31 set: a leaf, bit 30 set for a TLAS
+// leaf (instances start .. start + num - 1), bits 28-29 num - 1, bits 0-27 start (first instance,
+// triangle-pair record or quad record)
+struct alignas(16) DWide {
+    float4 r0;
+    uint4 r1, r2, r3;
+};
+enum : unsigned { W_EMPTY = 0xffffffffu, W_LEAF = 0x80000000u, W_INST = 0x40000000u, W_START = 0x0fffffffu };
 // Traversal record of an instance, 64 B: inverse(frame, true) as 12 floats + ids.
 struct alignas(16) DInstTrav {
     float4 i0, i1, i2;  // inv x.xyz y.x | y.yz z.xy | z.z o.xyz
@@ -108,6 +128,8 @@ struct alignas(16) DLight {
 
 struct DScene {
     const DNode* nodes;      // TLAS nodes, then every BLAS (global node indices)
+    const DWide* wnodes;     // the wide traversal's records: TLAS records, then every BLAS's
+    int tlas_wnodes;         // TLAS records (a record index below it is a TLAS record)
     const float4* prims;  // triangle pair: 5 float4 (p1, p2-p1, p3-p1 of two triangles interleaved,
                           // then both element ids); quad: 4 float4 (p1|elem, p2, p3, p4|p3==p4)
     const DInstTrav* inst_trav;
@@ -143,6 +165,7 @@ struct DScene {
     const float* byte_lut;  // byte_to_float(b)
     int tlas_nnodes, nenvs, nlights;
     int order_flip;  // jt_params.traversal: 0 the reference's child order, 7 the near child first
+                     // (near and wide)
     float light_pick_pdf;  // sample_uniform_pdf(nlights) = Float32(1 / nlights) (src/sampling.jl:31)
     int light_inline;  // every instance light's shape BVH is one leaf: light chains run inline (jtk::light_chain)
     // Small-scene mode: every array above that the traversal and shading read per step, packed
@@ -155,6 +178,7 @@ struct DScene {
     int ovf_stride;
     int ring;  // entries of the LDS ring in use (a power of two <= the kernel's RING)
     int stack_need;  // stack bound of the scene: LDS-mode kernels without overflow allocate this many
+    int o_wnodes;
     int o_nodes, o_prims, o_inst_trav, o_inst_blas, o_inst_shade, o_shapes;
     int o_pos, o_nrm, o_tc, o_col, o_elems, o_materials, o_lights, o_cdf, o_enrm, o_enrm_id;
     int o_light_hit, o_light_elems;

@@ -368,6 +368,7 @@ struct Trav {
     int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
     float h_u, h_v;
     int nh;              // hits accepted so far (every tmax change), saturating at 63
+    unsigned nxt;        // wide traversal: the child word visited by the next node step (W_EMPTY: pop)
 };
 
 __device__ __forceinline__ int neg_mask(v3 d, int flip) {
@@ -387,6 +388,17 @@ __device__ __forceinline__ Hit query_hit(const Trav& T) {
 }
 
 __device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T.nprim > 0; }
+// A lane's next step in either traversal: a primitive test (nprim > 0) or a node step (a stack
+// entry, or in the wide traversal a pending child word); neither: its query is done (sp 0) or the
+// lane has no samples left (sp < 0).
+template <bool WIDE>
+__device__ __forceinline__ bool wants_node(const Trav& T) {
+    return T.nprim == 0 && (T.sp > 0 || (WIDE && T.nxt != W_EMPTY));
+}
+template <bool WIDE>
+__device__ __forceinline__ bool query_done(const Trav& T) {
+    return (T.sp | T.nprim) == 0 && (!WIDE || T.nxt == W_EMPTY);
+}
 
 __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d, unsigned root, int* stack) {
     T.wo = o;
@@ -410,6 +422,41 @@ __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d
     stack[0] = (int)root;
     T.sp = 1;
     T.low = 0;
+    T.nxt = W_EMPTY;
+}
+// query_begin of the wide traversal: the root is the first node step's child word (the TLAS
+// root record, or an instance leaf of one instance for intersect_instance_bvh); the stack is empty
+__device__ __forceinline__ void query_begin_wide(const DScene& S, Trav& T, v3 o, v3 d, unsigned root_word) {
+    T.wo = o;
+    T.wd = d;
+    T.wdinv = V3(jl_rcp(d.x), jl_rcp(d.y), jl_rcp(d.z));  // ray_dinv (src/bvh.jl:322), no guard
+    T.lo = o;
+    T.ld = d;
+    T.ldinv = T.wdinv;
+    T.tmax = __builtin_inff();
+    T.nh = 0;
+    T.h_inst = -1;
+    T.h_elem = -1;
+    T.h_u = 0;
+    T.h_v = 0;
+    T.nprim = 0;
+    T.prim = 0;
+    T.cur_inst = -1;
+    T.cur_kind = KIND_TRI;
+    T.inst_space = 0;
+    T.negmask = neg_mask(d, S.order_flip);
+    T.sp = 0;
+    T.low = 0;
+    T.nxt = root_word;
+}
+constexpr unsigned WROOT_SCENE = 0u;  // the TLAS root record
+__device__ __forceinline__ unsigned wroot_instance(int inst) { return W_LEAF | W_INST | (unsigned)inst; }
+// query_begin for either traversal: a closest-hit scene query, or (inst >= 0) the
+// intersect_instance_bvh of sample_lights_pdf
+template <bool WIDE>
+__device__ __forceinline__ void query_start(const DScene& S, Trav& T, v3 o, v3 d, int inst, int* stack) {
+    if (WIDE) query_begin_wide(S, T, o, d, inst < 0 ? WROOT_SCENE : wroot_instance(inst));
+    else query_begin(S, T, o, d, inst < 0 ? ((T_TLAS << 30) | SNAP_NONE) : ((T_INST << 30) | SNAP_NONE | (unsigned)inst), stack);
 }
 
 // The current BLAS leaf's next primitive(s), in order (src/bvh.jl:444-484). Triangles go in
@@ -600,6 +647,127 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         T.prim = start;
         T.nprim = num;
     }
+}
+
+// ============================================================================ wide traversal
+// JT_TRAVERSAL_WIDE (DWide records, jt_device.h). The children of a record are visited in the
+// binary tree's DFS order for the ray: the near pair first by N's axis a0, in each pair the near
+// child by a1 / a2 — the same rule as the binary near-first order (S.order_flip folds the order
+// into negmask), so leaves are reached in the binary near-first sequence. flips bit 0: the R pair
+// first; bit 1 / 2: within L / R the second slot first. Visit index k -> slot:
+__device__ __forceinline__ int wide_slot(unsigned flips, int k) {
+    const int p = (k >> 1) ^ (int)(flips & 1u);
+    return 2 * p + ((k & 1) ^ (int)((flips >> (p ? 2 : 1)) & 1u));
+}
+__device__ __forceinline__ unsigned wide_word(const uint4& r3, int slot) {
+    return slot == 0 ? r3.x : slot == 1 ? r3.y : slot == 2 ? r3.z : r3.w;
+}
+// dequantised box of slot c (the record's origin + byte * scale, in float) as intersect_bbox's
+// (bmin.x, bmax.x, bmin.y, bmax.y), (bmin.z, bmax.z)
+__device__ __forceinline__ void wide_box(const float4& r0, const uint4& r1, const uint4& r2, float sx, float sy,
+                                         float sz, int c, float4& a, float4& b) {
+    const int sh = 8 * c;
+    a = make_float4(r0.x + (float)((r1.x >> sh) & 255u) * sx, r0.x + (float)((r1.y >> sh) & 255u) * sx,
+                    r0.y + (float)((r1.z >> sh) & 255u) * sy, r0.y + (float)((r1.w >> sh) & 255u) * sy);
+    b = make_float4(r0.z + (float)((r2.x >> sh) & 255u) * sz, r0.z + (float)((r2.y >> sh) & 255u) * sz, 0.0f, 0.0f);
+}
+// Stack entries of the wide traversal (32 bits): a group — the children of record `index` still
+// to visit (bit 31 clear; bits 28-30 the record's flips for this ray, 24-27 the visit-order mask
+// of children whose boxes passed, 0-23 the record) — or an instance range (bit 31 set; bits 24-25
+// count - 1, 0-23 the first instance) of a TLAS leaf whose first instance is being visited.
+// A child whose box passed is visited even if tmax has shrunk since (no re-test at pop).
+__device__ __forceinline__ void wide_take(Trav& T, unsigned w) {
+    if ((w & (W_LEAF | W_INST)) == W_LEAF) {  // a BLAS leaf: its primitives are tested next, in order
+        T.prim = (int)(w & W_START);
+        T.nprim = (int)((w >> 28) & 3u) + 1;
+    } else {
+        T.nxt = w;  // a record, or a TLAS leaf (its first instance is visited by the next step)
+    }
+}
+// one record visit: the up-to-four child boxes against the current ray and tmax; the first passing
+// child (visit order) is taken at once, the others are pushed as one group entry
+template <int RING, bool OVF, int COUNT>
+__device__ __forceinline__ void wide_visit(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt, unsigned idx) {
+    if (COUNT) cnt.nodes++;
+    const DWide& rec = S.wnodes[idx];
+    const float4 r0 = rec.r0;
+    const uint4 r1 = rec.r1, r2 = rec.r2, r3 = rec.r3;
+    const unsigned meta = __float_as_uint(r0.w);
+    const float sx = __uint_as_float((meta & 255u) << 23), sy = __uint_as_float(((meta >> 8) & 255u) << 23),
+                sz = __uint_as_float(((meta >> 16) & 255u) << 23);
+    unsigned hits = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        float4 a, b;
+        wide_box(r0, r1, r2, sx, sy, sz, c, a, b);
+        if (wide_word(r3, c) != W_EMPTY && intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, a, b)) hits |= 1u << c;
+    }
+    if (!hits) return;
+    const unsigned ax = meta >> 24;
+    const unsigned flips = ((T.negmask >> (ax & 3u)) & 1u ? 0u : 1u) | ((T.negmask >> ((ax >> 2) & 3u)) & 1u ? 0u : 2u) |
+                           ((T.negmask >> ((ax >> 4) & 3u)) & 1u ? 0u : 4u);
+    unsigned vm = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) vm |= ((hits >> wide_slot(flips, k)) & 1u) << k;
+    const int k0 = __builtin_ctz(vm);
+    const unsigned rest = vm & (vm - 1u);
+    if (rest) st_push<RING, OVF>(S, T, stack, pixel, flips << 28 | rest << 24 | idx);
+    wide_take(T, wide_word(r3, wide_slot(flips, k0)));
+}
+// One node step of the wide traversal: the pending child word, or the next child of the group on
+// top of the stack (its word: one 4-B load), or the next instance of a range. An instance visit
+// (inverse frame precomputed, src/bvh.jl:345,502) and the visit of its BLAS root record are one
+// step, as in the binary traversal.
+template <int RING, bool OVF, int COUNT, int F>
+__device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
+    constexpr bool XF = (F & FT_XFORM) != 0;
+    unsigned w = T.nxt;
+    if (w == W_EMPTY) {
+        const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
+        const unsigned idx = e & IDX_MASK;
+        if (!(e >> 31)) {  // a group: its next child in visit order
+            const unsigned m = (e >> 24) & 15u;
+            const unsigned rest = m & (m - 1u);
+            if (rest) st_push<RING, OVF>(S, T, stack, pixel, (e & ~(15u << 24)) | rest << 24);
+            if (XF && T.inst_space && idx < (unsigned)S.tlas_wnodes) world_ray(S, T);  // back in the TLAS
+            w = reinterpret_cast<const unsigned*>(S.wnodes + idx)[12 + wide_slot((e >> 28) & 7u, __builtin_ctz(m))];
+            if ((w & (W_LEAF | W_INST)) == W_LEAF) {
+                wide_take(T, w);
+                return;
+            }
+        } else {  // the rest of a TLAS leaf's instances
+            w = W_LEAF | W_INST | ((e >> 24) & 3u) << 28 | idx;
+        }
+    } else {
+        T.nxt = W_EMPTY;
+    }
+    if (w & W_LEAF) {  // a TLAS leaf: visit its first instance, keep the others as a range entry
+        const unsigned inst = w & W_START, n1 = (w >> 28) & 3u;
+        if (n1) st_push<RING, OVF>(S, T, stack, pixel, W_LEAF | (n1 - 1u) << 24 | (inst + 1u));
+        if (COUNT) cnt.instances++;
+        const int4 ib = S.inst_blas[inst];  // wide BLAS root record, identity, kind, shape
+        if (!XF || ib.y) {
+            if (XF && T.inst_space) world_ray(S, T);
+        } else {
+            const DInstTrav it = S.inst_trav[inst];
+            const fr3 inv = frame_from(it.i0, it.i1, it.i2);
+            T.lo = transform_point(inv, T.wo);
+            T.ld = transform_vector(inv, T.wd);
+            T.ldinv = V3(jl_rcp(T.ld.x), jl_rcp(T.ld.y), jl_rcp(T.ld.z));
+            T.negmask = neg_mask(T.ld, S.order_flip);
+            T.inst_space = 1;
+        }
+        T.cur_inst = (int)inst;
+        T.cur_kind = ib.z;
+        w = (unsigned)ib.x;
+    }
+    wide_visit<RING, OVF, COUNT>(S, T, stack, pixel, cnt, w);
+}
+// a node step in either traversal
+template <bool WIDE, int RING, bool OVF, int COUNT, bool NCACHE, int F>
+__device__ __forceinline__ void node_step_any(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
+    if (WIDE) node_step_wide<RING, OVF, COUNT, F>(S, T, stack, pixel, cnt);
+    else node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
 }
 
 // ============================================================================ lights (src/trace.jl)
@@ -862,13 +1030,13 @@ __device__ __forceinline__ bool light_hit(const DScene& S, const DParams& P, Pat
 // here, where most of the wave's lanes run their chains side by side, instead of one-prim-step
 // queries and light-hit steps of a few lanes inside the traversal phase. Returns light_hit's
 // "path done"; otherwise st.phase is PH_SCENE (the next bounce's scene query).
-template <int RING, bool OVF, int COUNT, bool NCACHE, int F, class CountLq>
+template <bool WIDE, int RING, bool OVF, int COUNT, bool NCACHE, int F, class CountLq>
 __device__ __forceinline__ bool light_chain(const DScene& S, const DParams& P, Path& st, Trav& T, int* stack, int pixel,
                                             Counters& cnt, CountLq count_lq) {
     do {
         count_lq();
-        query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
-        node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);  // instance + its one-leaf root
+        query_start<WIDE>(S, T, st.o, st.d, S.lights[st.li].instance, stack);
+        node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);  // instance + its one-leaf root
         while (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
         if (light_hit<F>(S, P, st, query_hit(T))) return true;
     } while (st.phase == PH_LIGHT);
@@ -1194,7 +1362,7 @@ __device__ __forceinline__ int opaque_lane_id() {
 // trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
 // 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
 // mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, bool WIDE>
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
                                            int* stack) {
     const int lane = threadIdx.x & 63;
@@ -1285,9 +1453,10 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     // sp > 0 in a query, sp == nprim == 0 waiting for the shading phase
     T.sp = -1;
     T.nprim = 0;
+    T.nxt = W_EMPTY;
     if (alive) {
         start_path<F>(P, i, j, pixel, sample, st);
-        query_begin(S, T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
+        query_start<WIDE>(S, T, st.o, st.d, -1, stack);
     }
     if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(alive));
     else lds_count(1, alive);
@@ -1306,8 +1475,8 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
         constexpr bool LSTEP = light_steps(SAMPLER, F);
         for (;;) {
             const bool wantp = T.nprim > 0;
-            const bool wantn = T.nprim == 0 && T.sp > 0;
-            const bool waiting = (T.sp | T.nprim) == 0;
+            const bool wantn = wants_node<WIDE>(T);
+            const bool waiting = query_done<WIDE>(T);
             const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
             const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
             int nw = lane_count(__builtin_amdgcn_ballot_w64(waiting));
@@ -1323,11 +1492,11 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                         } else if (st.phase == PH_LIGHT) {
                             if (WC) c_lq = true;
                             else lds_count(2, true);
-                            query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
+                            query_start<WIDE>(S, T, st.o, st.d, S.lights[st.li].instance, stack);
                         } else {
                             if (WC) c_ray = true;
                             else lds_count(1, true);
-                            query_begin(S, T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
+                            query_start<WIDE>(S, T, st.o, st.d, -1, stack);
                         }
                     }
                     if (WC) {
@@ -1360,7 +1529,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 constexpr int NREP = ft_none(F) ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
 #pragma unroll
                 for (int k = 0; k < NREP; k++)
-                    if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
             }
         }
 #if JT_STAMPS
@@ -1374,7 +1543,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #if JT_STAMPS
         {
             int mid = -1, mt = -1;
-            if ((T.sp | T.nprim) == 0 && st.phase == PH_SCENE && T.h_inst >= 0) {
+            if (query_done<WIDE>(T) && st.phase == PH_SCENE && T.h_inst >= 0) {
                 mid = S.inst_shade[T.h_inst].material;
                 mt = (F & FT_MAT) ? S.materials[mid].type : (int)M_MATTE;
             }
@@ -1392,7 +1561,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
             }
         }
 #endif
-        if ((T.sp | T.nprim) == 0) {
+        if (query_done<WIDE>(T)) {
             bool alive = true;
             // no light query ever leaves the shading phase (FT_LINL), or none exists (FT_NOIL)
             constexpr bool LINL = (F & (FT_LINL | FT_NOIL)) != 0;
@@ -1419,7 +1588,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
             if (SAMPLER == 1 && !done && st.phase == PH_LIGHT && chains_inline(F, S)) {
                 unsigned nlq = 0;
-                done = light_chain<RING, OVF, COUNT, NCACHE, F>(S, P, st, T, stack, pixel, cnt, [&] {
+                done = light_chain<WIDE, RING, OVF, COUNT, NCACHE, F>(S, P, st, T, stack, pixel, cnt, [&] {
                     if (WC) nlq++;
                     else lds_count(2, true);
                 });
@@ -1477,17 +1646,17 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 if (SAMPLER == 1 && !LINL && st.phase == PH_LIGHT) {
                     if (WC) c_lq = true;
                     else lds_count(2, true);
-                    query_begin(S, T, st.o, st.d, (T_INST << 30) | SNAP_NONE | (unsigned)S.lights[st.li].instance, stack);
+                    query_start<WIDE>(S, T, st.o, st.d, S.lights[st.li].instance, stack);
                 } else {
                     if (WC) c_ray = true;
                     else lds_count(1, true);
-                    query_begin(S, T, st.o, st.d, (T_TLAS << 30) | SNAP_NONE, stack);
+                    query_start<WIDE>(S, T, st.o, st.d, -1, stack);
                 }
                 // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
                 // where most of the wave's lanes take part, rather than in a sparser traversal step
 #pragma unroll
                 for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
-                    if (T.nprim == 0 && T.sp > 0) node_step<RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
             }
 #if JT_STAMPS
             t_qb += __builtin_amdgcn_s_memtime() - s3;
@@ -1578,6 +1747,7 @@ __host__ __device__ constexpr size_t lds_stack_bytes(bool ovf, int ring, int nee
 __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob) {
     DScene L = S;
     L.nodes = reinterpret_cast<const DNode*>(blob + S.o_nodes);
+    L.wnodes = reinterpret_cast<const DWide*>(blob + S.o_wnodes);
     L.prims = reinterpret_cast<const float4*>(blob + S.o_prims);
     L.inst_trav = reinterpret_cast<const DInstTrav*>(blob + S.o_inst_trav);
     L.inst_blas = reinterpret_cast<const int4*>(blob + S.o_inst_blas);
@@ -1599,16 +1769,16 @@ __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob)
 }
 
 // HBM mode: the scene is read from global memory (L2/MALL-resident); stack in static LDS.
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool WIDE>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     __shared__ int lds_stack[RING * BLOCK];
-    trace_body<SAMPLER, RING, OVF, COUNT, F, true>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
+    trace_body<SAMPLER, RING, OVF, COUNT, F, true, WIDE>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
 }
 
 // LDS mode (small scenes): the workgroup stages the scene blob into LDS once; every node,
 // instance, primitive and shading record is then a ds_read instead of a vector-memory load
 // through the TA/TD path (the measured limiter of the HBM-mode kernel).
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool WIDE>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     extern __shared__ uint4 dyn_lds[];
     // the stack takes the first bytes (lds_stack_bytes), the blob follows
@@ -1616,13 +1786,13 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(D
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
     const DScene L = blob_scene(S, blob);
-    trace_body<SAMPLER, RING, OVF, COUNT, F, false>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+    trace_body<SAMPLER, RING, OVF, COUNT, F, false, WIDE>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of
 // tiles), each wave then pulls work units until the launch's units are exhausted.
 // LDSK: the specialisation also has an LDS-mode kernel (the large-scene masks run in HBM mode).
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool LDSK = true>
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool LDSK, bool WIDE>
 hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
     const int tiles = launch_tiles(P);
     const int want = (tiles + BLOCK / 64 - 1) / (BLOCK / 64);
@@ -1632,18 +1802,18 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
     if constexpr (LDSK) {
         if (S.blob_n16 > 0) {
         const size_t lds = lds_stack_bytes(OVF, RING, S.stack_need) + (size_t)S.blob_n16 * 16;
-        const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>;
+        const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F, WIDE>;
         if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
         const int nwg = std::min(want, per_cu * cus);
-        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
+        hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F, WIDE>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
         return hipGetLastError();
         }
     }
-    const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT, F>;
+    const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT, F, WIDE>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     const int nwg = std::min(want, per_cu * cus);
-    hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
+    hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F, WIDE>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
     return hipGetLastError();
 }
 
@@ -1668,18 +1838,25 @@ inline int kernel_mask(int feat, int need, int ring, bool lds, bool linl, bool i
     return FT_ALL;
 }
 
-// Kernel configurations: (stack ring, HBM overflow, feature mask, LDS-mode kernel too). Each is
-// compiled in its own translation unit (jt_kv.hip with JT_VARIANT = its index) for both
-// samplers and both counter levels; launch_s (jt_trace.hip) dispatches among them.
+// Kernel configurations: (stack ring, HBM overflow, feature mask, LDS-mode kernel too), each in
+// the binary traversal (ID 0-7) and the wide one (ID + 8, JT_TRAVERSAL_WIDE). Each is compiled
+// in its own translation unit (jt_kv.hip with JT_VARIANT = its index) for both samplers and both
+// counter levels; launch_s (jt_trace.hip) dispatches among them.
+constexpr int NUM_BASE_CONFIGS = 8;
 template <int ID>
 struct LaunchConfig;
-#define JT_LAUNCH_CONFIG(ID, R, O, F, L)                 \
-    template <>                                           \
-    struct LaunchConfig<ID> {                             \
-        static constexpr int ring = R;                    \
-        static constexpr bool ovf = O;                    \
-        static constexpr int feat = F;                    \
-        static constexpr bool lds = L;                    \
+#define JT_LAUNCH_CONFIG(ID, R, O, F, L)                            \
+    template <>                                                      \
+    struct LaunchConfig<ID> {                                        \
+        static constexpr int ring = R;                               \
+        static constexpr bool ovf = O;                               \
+        static constexpr int feat = F;                               \
+        static constexpr bool lds = L;                               \
+        static constexpr bool wide = false;                          \
+    };                                                               \
+    template <>                                                      \
+    struct LaunchConfig<ID + NUM_BASE_CONFIGS> : LaunchConfig<ID> {  \
+        static constexpr bool wide = true;                           \
     };
 JT_LAUNCH_CONFIG(0, 16, false, FT_NONE | FT_LINL, true)  // small scenes, matte triangles (cornellbox)
 JT_LAUNCH_CONFIG(1, 16, false, FT_ALL, true)             // small scenes, any features
@@ -1690,12 +1867,12 @@ JT_LAUNCH_CONFIG(5, 16, true, FT_ALL, true)              // deep BVHs, any featu
 JT_LAUNCH_CONFIG(6, 32, true, FT_ALL, true)              // a 32-entry LDS ring (JT_LDS_STACK)
 JT_LAUNCH_CONFIG(7, 16, false, FT_NONE, true)            // matte triangles, light chains through the traversal
 #undef JT_LAUNCH_CONFIG
-constexpr int NUM_LAUNCH_CONFIGS = 8;
+constexpr int NUM_LAUNCH_CONFIGS = 2 * NUM_BASE_CONFIGS;
 
 template <int ID, int SAMPLER, int COUNT>
 hipError_t launch_cfg(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
     using C = LaunchConfig<ID>;
-    return launch_t<SAMPLER, C::ring, C::ovf, COUNT, C::feat, C::lds>(S, P, s0, s1, A, st, cus);
+    return launch_t<SAMPLER, C::ring, C::ovf, COUNT, C::feat, C::lds, C::wide>(S, P, s0, s1, A, st, cus);
 }
 // explicit instantiation (JT_KV_INSTANTIATE, in jt_kv.hip) or declaration (elsewhere) of one
 // configuration for both samplers and both counter levels

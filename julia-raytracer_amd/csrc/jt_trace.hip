@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -29,25 +30,39 @@ JT_KV_FOR(4, extern template)
 JT_KV_FOR(5, extern template)
 JT_KV_FOR(6, extern template)
 JT_KV_FOR(7, extern template)
+JT_KV_FOR(8, extern template)
+JT_KV_FOR(9, extern template)
+JT_KV_FOR(10, extern template)
+JT_KV_FOR(11, extern template)
+JT_KV_FOR(12, extern template)
+JT_KV_FOR(13, extern template)
+JT_KV_FOR(14, extern template)
+JT_KV_FOR(15, extern template)
 
+// configuration ID of the binary traversal, or its wide twin (ID + NUM_BASE_CONFIGS)
+template <int ID, int SAMPLER, int COUNT>
+hipError_t launch_tw(bool wide, const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
+    return wide ? launch_cfg<ID + NUM_BASE_CONFIGS, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus)
+                : launch_cfg<ID, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+}
 // Stack configurations: the whole bound in a 16-entry LDS ring, or a RING-entry ring + HBM.
 template <int SAMPLER, int COUNT>
-hipError_t launch_s(int need, int ring, int kmask, const DScene& S, const DParams& P, int s0, int s1,
+hipError_t launch_s(int need, int ring, int kmask, bool wide, const DScene& S, const DParams& P, int s0, int s1,
                     const DAccum& A, hipStream_t st, int cus) {
     if (need <= 16) {
-        if (kmask == (FT_NONE | FT_LINL)) return launch_cfg<0, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
-        if (kmask == FT_NONE) return launch_cfg<7, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
-        return launch_cfg<1, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+        if (kmask == (FT_NONE | FT_LINL)) return launch_tw<0, SAMPLER, COUNT>(wide, S, P, s0, s1, A, st, cus);
+        if (kmask == FT_NONE) return launch_tw<7, SAMPLER, COUNT>(wide, S, P, s0, s1, A, st, cus);
+        return launch_tw<1, SAMPLER, COUNT>(wide, S, P, s0, s1, A, st, cus);
     }
     if (ring <= 16) {
         switch (kmask) {
-            case FT_MESH | FT_LINL: return launch_cfg<2, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
-            case FT_MESH_ENV | FT_NOIL: return launch_cfg<3, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
-            case FT_MESH_ENV_QUAD | FT_LINL: return launch_cfg<4, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
-            default: return launch_cfg<5, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+            case FT_MESH | FT_LINL: return launch_tw<2, SAMPLER, COUNT>(wide, S, P, s0, s1, A, st, cus);
+            case FT_MESH_ENV | FT_NOIL: return launch_tw<3, SAMPLER, COUNT>(wide, S, P, s0, s1, A, st, cus);
+            case FT_MESH_ENV_QUAD | FT_LINL: return launch_tw<4, SAMPLER, COUNT>(wide, S, P, s0, s1, A, st, cus);
+            default: return launch_tw<5, SAMPLER, COUNT>(wide, S, P, s0, s1, A, st, cus);
         }
     }
-    return launch_cfg<6, SAMPLER, COUNT>(S, P, s0, s1, A, st, cus);
+    return launch_tw<6, SAMPLER, COUNT>(wide, S, P, s0, s1, A, st, cus);
 }
 }  // namespace jtk
 
@@ -71,6 +86,7 @@ struct jt_ctx {
     int ring = 16;
     int feat = FT_ALL;   // scene feature bits (jt_device.h)
     int kmask = FT_ALL;  // feature mask of the kernel specialisation the scene runs
+    bool wide = false;   // JT_TRAVERSAL_WIDE: the wide-record kernels (configurations 8-15)
     int first = -1, next = 0;  // running-mean origin and next expected sample
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     bool failed = false;       // a launch's tile-order wait timed out: the running means are unusable
@@ -225,6 +241,114 @@ bool rot_identity(const float* fv) {
 DNode pack_node(const jt_bvh_node& n, int start) {
     unsigned meta = (unsigned)(uint16_t)n.num | ((unsigned)(uint8_t)n.axis << 16) | ((unsigned)(n.internal ? 1 : 0) << 24);
     return DNode{f4(n.bmin[0], n.bmax[0], n.bmin[1], n.bmax[1]), f4(n.bmin[2], n.bmax[2], as_f(start), as_f(meta))};
+}
+
+// ------------------------------------------------------------- wide records (JT_TRAVERSAL_WIDE)
+// Conservative 8-bit quantisation of a child's slab [cmin, cmax] on one axis, relative to the
+// record's origin o with scale s (a power of two): the largest lo with o + lo * s <= cmin and the
+// smallest hi with o + hi * s >= cmax, evaluated in the device's float operations (wide_box,
+// jt_kernels.h; -ffp-contract=off on both sides). false: no byte fits at this scale.
+bool quantize_axis(float o, float s, float cmin, float cmax, unsigned& lo, unsigned& hi) {
+    auto deq = [&](int q) { return o + (float)q * s; };
+    int q = (int)std::max(0.0, std::min(255.0, std::floor(((double)cmin - (double)o) / (double)s)));
+    while (q > 0 && deq(q) > cmin) q--;
+    while (q < 255 && deq(q + 1) <= cmin) q++;
+    if (!(deq(q) <= cmin)) return false;
+    lo = (unsigned)q;
+    q = (int)std::max(0.0, std::min(255.0, std::ceil(((double)cmax - (double)o) / (double)s)));
+    while (q < 255 && deq(q) < cmax) q++;
+    while (q > 0 && deq(q - 1) >= cmax) q--;
+    if (!(deq(q) >= cmax)) return false;
+    hi = (unsigned)q;
+    return true;
+}
+float exp_scale(int e) {  // 2^(e - 127), e = a normal float's biased exponent
+    const unsigned b = (unsigned)e << 23;
+    float f;
+    std::memcpy(&f, &b, 4);
+    return f;
+}
+// The wide records of one binary tree, appended to `out` breadth-first (global indices =
+// positions in `out`). A record stands for an internal node N (or the root leaf) and holds N's
+// grandchildren in slots [LL, LR, RL, RR] (a leaf child takes the pair's first slot alone), their
+// boxes quantised relative to N's box per axis at the smallest scale 2^(e-127) >= extent / 255
+// (and the next larger ones until every child fits). leaf_word(k): the child word of binary leaf
+// k. Returns the root record's index, or -1 with the error set.
+int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_word, std::vector<DWide>& out) {
+    if (t.nnodes <= 0) return jt::fail(JT_ERR_INVALID, "wide traversal: empty BVH"), -1;
+    std::vector<int> q{0}, rec{(int)out.size()};
+    out.emplace_back();
+    for (size_t h = 0; h < q.size(); h++) {
+        const jt_bvh_node& N = t.nodes[q[h]];
+        int slot[4] = {-1, -1, -1, -1}, a1 = 0, a2 = 0;
+        if (!N.internal) {
+            slot[0] = q[h];
+        } else {
+            const int L = N.start, R = N.start + 1;
+            if (t.nodes[L].internal) {
+                slot[0] = t.nodes[L].start;
+                slot[1] = t.nodes[L].start + 1;
+                a1 = t.nodes[L].axis;
+            } else {
+                slot[0] = L;
+            }
+            if (t.nodes[R].internal) {
+                slot[2] = t.nodes[R].start;
+                slot[3] = t.nodes[R].start + 1;
+                a2 = t.nodes[R].axis;
+            } else {
+                slot[2] = R;
+            }
+        }
+        unsigned word[4] = {W_EMPTY, W_EMPTY, W_EMPTY, W_EMPTY};
+        for (int c = 0; c < 4; c++) {
+            if (slot[c] < 0) continue;
+            const jt_bvh_node& C = t.nodes[slot[c]];
+            if (C.internal) {
+                if (out.size() >= (size_t)IDX_MASK) return jt::fail(JT_ERR_UNSUPPORTED, "scene exceeds 2^24 wide records"), -1;
+                word[c] = (unsigned)out.size();
+                q.push_back(slot[c]);
+                rec.push_back((int)out.size());
+                out.emplace_back();
+            } else {
+                if (C.num < 1 || C.num > 4) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: a BVH leaf outside 1..4 primitives"), -1;
+                word[c] = leaf_word(slot[c]);
+                if (word[c] == W_EMPTY) return -1;
+            }
+        }
+        // quantisation per axis
+        unsigned e3[3], lo[3][4] = {}, hi[3][4] = {};
+        for (int ax = 0; ax < 3; ax++) {
+            const float o = N.bmin[ax];
+            bool finite = std::isfinite(N.bmin[ax]) && std::isfinite(N.bmax[ax]);
+            for (int c = 0; c < 4; c++)
+                if (slot[c] >= 0)
+                    finite = finite && std::isfinite(t.nodes[slot[c]].bmin[ax]) && std::isfinite(t.nodes[slot[c]].bmax[ax]);
+            if (!finite) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: a non-finite BVH box"), -1;
+            const double ext = (double)N.bmax[ax] - (double)N.bmin[ax];
+            int e = 1;  // smallest biased exponent with 255 * 2^(e - 127) >= ext
+            while (e < 254 && 255.0 * std::ldexp(1.0, e - 127) < ext) e++;
+            for (;; e++) {
+                if (e > 254) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: a box cannot be quantised"), -1;
+                const float sc = exp_scale(e);
+                bool ok = std::isfinite(o + 255.0f * sc);
+                for (int c = 0; c < 4 && ok; c++)
+                    if (slot[c] >= 0)
+                        ok = quantize_axis(o, sc, t.nodes[slot[c]].bmin[ax], t.nodes[slot[c]].bmax[ax], lo[ax][c], hi[ax][c]);
+                if (ok) break;
+            }
+            e3[ax] = (unsigned)e;
+        }
+        auto bytes = [](const unsigned* v) { return v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24; };
+        DWide& W = out[rec[h]];
+        const unsigned meta = e3[0] | e3[1] << 8 | e3[2] << 16 |
+                              ((unsigned)(N.internal ? N.axis : 0) | (unsigned)a1 << 2 | (unsigned)a2 << 4) << 24;
+        W.r0 = make_float4(N.bmin[0], N.bmin[1], N.bmin[2], as_f(meta));
+        W.r1 = make_uint4(bytes(lo[0]), bytes(hi[0]), bytes(lo[1]), bytes(hi[1]));
+        W.r2 = make_uint4(bytes(lo[2]), bytes(hi[2]), 0u, 0u);
+        W.r3 = make_uint4(word[0], word[1], word[2], word[3]);
+    }
+    return rec[0];
 }
 
 int check_tree(const jt_bvh_tree& t, int nprims_expected, const char* what) {
@@ -457,6 +581,9 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     std::vector<float2> tc;
     std::vector<int4> elems;
     std::vector<float4> enrm, enrm_id;
+    // the record (pair / quad) where each binary BLAS leaf's primitives start: the wide records'
+    // leaf words (JT_TRAVERSAL_WIDE)
+    std::vector<std::vector<int>> leaf_rec(scene->nshapes);
     for (int s = 0; s < scene->nshapes; s++) {
         const jt_shape& sh = scene->shapes[s];
         const jt_bvh_tree& t = bvh->blas[s];
@@ -492,6 +619,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                 col.push_back(f4(sh.colors[4 * v], sh.colors[4 * v + 1], sh.colors[4 * v + 2], sh.colors[4 * v + 3]));
         }
         const int nel = d.kind == KIND_TRI ? sh.ntriangles : sh.nquads;
+        leaf_rec[s].assign(t.nnodes, -1);
         // element normals (triangle_normal / quad_normal, src/geometry.jl:260-271) and their
         // transform_normal by an unrotated frame: host float ops identical to the device's
         for (int k = 0; k < nel; k++) {
@@ -529,6 +657,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                     continue;
                 }
                 blas.push_back(pack_node(n, d.prim_base + pairs));
+                leaf_rec[s][k] = d.prim_base + pairs;
                 for (int q = 0; q < n.num; q += 2) {
                     float4 p[2], e1[2], e2[2];
                     int el[2] = {-1, -1};
@@ -555,6 +684,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         for (int k = 0; k < t.nnodes; k++) {
             const jt_bvh_node& n = t.nodes[k];
             blas.push_back(pack_node(n, n.internal ? d.blas_root + n.start : d.prim_base + n.start));
+            if (!n.internal) leaf_rec[s][k] = d.prim_base + n.start;
         }
         // quad records in BVH leaf order (the reference reads positions through
         // bvh.primitives[i]; the records hold the same floats, pre-gathered)
@@ -569,6 +699,33 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             prims.push_back(b);
             prims.push_back(cc);
             prims.push_back(dd);
+        }
+    }
+    // wide records (JT_TRAVERSAL_WIDE): the TLAS's, then every BLAS's; the binary node array is
+    // then not uploaded
+    if (params->traversal != JT_TRAVERSAL_REFERENCE && params->traversal != JT_TRAVERSAL_NEAR &&
+        params->traversal != JT_TRAVERSAL_WIDE)
+        return bail(jt::fail(JT_ERR_INVALID, "traversal must be 0 (reference), 1 (near) or 2 (wide)"));
+    c->wide = params->traversal == JT_TRAVERSAL_WIDE;
+    std::vector<DWide> wnodes;
+    std::vector<int> wroot(scene->nshapes, 0);
+    int tlas_wnodes = 0;
+    if (c->wide) {
+        const int r = build_wide(bvh->tlas, [&](int k) -> unsigned {
+            const jt_bvh_node& n = bvh->tlas.nodes[k];
+            if (n.start < 0 || n.start > (int)W_START - 1) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: instance id too large"), (unsigned)W_EMPTY;
+            return W_LEAF | W_INST | (unsigned)(n.num - 1) << 28 | (unsigned)n.start;
+        }, wnodes);
+        if (r < 0) return bail(JT_ERR_UNSUPPORTED);
+        tlas_wnodes = (int)wnodes.size();
+        for (int s = 0; s < scene->nshapes; s++) {
+            const jt_bvh_tree& t = bvh->blas[s];
+            wroot[s] = build_wide(t, [&](int k) -> unsigned {
+                const int st0 = leaf_rec[s][k];
+                if (st0 < 0 || st0 > (int)W_START - 1) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: too many primitive records"), (unsigned)W_EMPTY;
+                return W_LEAF | (unsigned)(t.nodes[k].num - 1) << 28 | (unsigned)st0;
+            }, wnodes);
+            if (wroot[s] < 0) return bail(JT_ERR_UNSUPPORTED);
         }
     }
     std::vector<DInstTrav> itrav(scene->ninstances);
@@ -590,7 +747,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         const float idm[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
         bool ident = true;
         for (int q = 0; q < 12; q++) ident = ident && iv[q] == idm[q];
-        iblas[k] = make_int4(d.blas_root, ident ? 1 : 0, d.kind, in.shape);  // jtk::node_step reads x, y (z)
+        // jtk::node_step reads x, y (z); the wide traversal's x is the BLAS's root record
+        iblas[k] = make_int4(c->wide ? wroot[in.shape] : d.blas_root, ident ? 1 : 0, d.kind, in.shape);
         if (!ident) c->feat |= FT_XFORM;
         ishade[k] = DInstShade{f4(fv[0], fv[1], fv[2], fv[3]), f4(fv[4], fv[5], fv[6], fv[7]), f4(fv[8], fv[9], fv[10], fv[11]),
                                in.material, in.shape, scene->materials[in.material].type,
@@ -725,12 +883,15 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     DScene& S = c->S;
     // one zero record past the last primitive: prim_step reads the record after a leaf's last
     for (int q = 0; q < 4; q++) prims.push_back(f4(0, 0, 0, 0));
-    std::vector<DNode> nodes(tlas);
-    nodes.insert(nodes.end(), blas.begin(), blas.end());
+    std::vector<DNode> nodes;
+    if (!c->wide) {
+        nodes = tlas;
+        nodes.insert(nodes.end(), blas.begin(), blas.end());
+    }
     // traversal stack entries carry a 24-bit node / instance index (IDX_MASK)
     if (nodes.size() > IDX_MASK || (size_t)scene->ninstances > IDX_MASK)
         return bail(jt::fail(JT_ERR_UNSUPPORTED, "scene exceeds 2^24 BVH nodes or instances"));
-    if ((st = upload(c, nodes, &S.nodes)) || (st = upload(c, prims, &S.prims)) ||
+    if ((st = upload(c, nodes, &S.nodes)) || (st = upload(c, wnodes, &S.wnodes)) || (st = upload(c, prims, &S.prims)) ||
         (st = upload(c, itrav, &S.inst_trav)) || (st = upload(c, iblas, &S.inst_blas)) || (st = upload(c, ishade, &S.inst_shade)) ||
         (st = upload(c, shapes, &S.shapes)) || (st = upload(c, pos, &S.pos)) || (st = upload(c, nrm, &S.nrm)) ||
         (st = upload(c, tc, &S.tc)) || (st = upload(c, col, &S.col)) || (st = upload(c, elems, &S.elems)) ||
@@ -740,9 +901,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
         return bail(st);
     S.tlas_nnodes = (int)tlas.size();
-    if (params->traversal != JT_TRAVERSAL_REFERENCE && params->traversal != JT_TRAVERSAL_NEAR)
-        return bail(jt::fail(JT_ERR_INVALID, "traversal must be 0 (reference) or 1 (near)"));
-    S.order_flip = params->traversal == JT_TRAVERSAL_NEAR ? 7 : 0;
+    S.tlas_wnodes = tlas_wnodes;
+    S.order_flip = params->traversal == JT_TRAVERSAL_REFERENCE ? 0 : 7;  // near and wide: near child first
     S.nenvs = scene->nenvironments;
     S.nlights = lights->nlights;
     S.light_pick_pdf = lights->nlights > 0 ? (float)(1.0 / (double)lights->nlights) : 0.0f;
@@ -775,6 +935,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             return off;
         };
         S.o_nodes = add(nodes.data(), nodes.size() * sizeof(DNode));
+        S.o_wnodes = add(wnodes.data(), wnodes.size() * sizeof(DWide));
         S.o_prims = add(prims.data(), prims.size() * sizeof(float4));
         S.o_inst_trav = add(itrav.data(), itrav.size() * sizeof(DInstTrav));
         S.o_inst_blas = add(iblas.data(), iblas.size() * sizeof(int4));
@@ -1079,11 +1240,11 @@ int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
     if ((e = hipMemsetAsync(c->A.counters + 7, 0, 8, c->stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if (c->sampler == JT_SAMPLER_NAIVE)
-        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<2, 0>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<2, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     else
-        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<1, 0>(c->stack, c->ring, c->kmask, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<1, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     return JT_OK;
@@ -1372,10 +1533,11 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
         std::snprintf(filt, sizeof filt, " tile_filter=%d/%d ring_used=%d", c->P.tile_offset, c->P.tile_stride, c->S.ring);
     char tmp[640];
     std::snprintf(tmp, sizeof tmp,
-                  "kernel=%s<%d,%d,%s,%d,%d> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
+                  "kernel=%s<%d,%d,%s,%d,%d,%s> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
                   "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d env_alias=%d light_inline=%d%s",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
-                  ring, ovf ? "true" : "false", c->count, c->kmask, c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
+                  ring, ovf ? "true" : "false", c->count, c->kmask, c->wide ? "true" : "false",
+                  c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
                   c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->P.nct, c->tiles, BLOCK,
                   c->env_alias ? 1 : 0, c->S.light_inline, filt);
     std::snprintf(buf, (size_t)n, "%s", tmp);

@@ -12,6 +12,11 @@ computed by one sum-reduce (RCCL over xGMI with backend "nccl"; gloo on CPU in t
 """
 from __future__ import annotations
 
+import json
+from pathlib import Path
+
+import numpy as np
+
 
 def shard_range(total_samples: int, world: int, rank: int) -> tuple[int, int]:
     return rank * total_samples // world, (rank + 1) * total_samples // world
@@ -32,3 +37,52 @@ def all_reduce_running_means(tensor, n_local: int, n_total: int, dist):
     dist.all_reduce(part, op=dist.ReduceOp.SUM)
     part /= float(n_total)
     return part
+
+
+# ------------------------------------------------------------------ reduced-image check
+# The multi-rank bench proves its reduce with a deterministic fingerprint of the image: block means
+# of the final running-mean RGBA, committed once per workload from a one-GPU run
+# (profiles/image_signatures.json) and compared by rank 0 after every run. A sample split equals the
+# one-device image up to fp32 summation order (~1e-6 relative), so block means agree to ~1e-6; a
+# missing or doubled shard, a wrong weight or a stale buffer moves them by percents.
+SIGNATURE_BLOCK = 40
+SIGNATURE_RTOL = 1e-4
+SIGNATURE_ATOL = 1e-6
+
+
+def image_signature(img, block: int = SIGNATURE_BLOCK) -> np.ndarray:
+    """Block means (float64) of an (H, W, 4) image over block x block pixels (edge blocks partial)."""
+    a = np.asarray(img, np.float64)
+    H, W = a.shape[:2]
+    hb, wb = -(-H // block), -(-W // block)
+    out = np.zeros((hb, wb, a.shape[2]))
+    for i in range(hb):
+        for j in range(wb):
+            out[i, j] = a[i * block:(i + 1) * block, j * block:(j + 1) * block].mean(axis=(0, 1))
+    return out
+
+
+def load_signature(path, key: str):
+    p = Path(path)
+    if not p.exists():
+        return None
+    d = json.loads(p.read_text()).get(key)
+    return None if d is None else np.asarray(d["blocks"], np.float64)
+
+
+def save_signature(path, key: str, sig: np.ndarray, note: str):
+    p = Path(path)
+    d = json.loads(p.read_text()) if p.exists() else {}
+    d[key] = {"block": SIGNATURE_BLOCK, "note": note, "blocks": np.round(sig, 9).tolist()}
+    p.write_text(json.dumps(d, indent=0, sort_keys=True))
+
+
+def compare_signature(sig: np.ndarray, ref: np.ndarray) -> dict:
+    """max relative error of the block means against the reference, and whether it is within
+    SIGNATURE_RTOL (+ SIGNATURE_ATOL for near-black blocks)."""
+    if sig.shape != ref.shape:
+        return {"ok": False, "max_rel": None, "why": f"shape {sig.shape} vs reference {ref.shape}"}
+    err = np.abs(sig - ref)
+    ok = bool(np.all(err <= SIGNATURE_RTOL * np.abs(ref) + SIGNATURE_ATOL))
+    rel = float(np.max(err / np.maximum(np.abs(ref), SIGNATURE_ATOL)))
+    return {"ok": ok, "max_rel": rel}

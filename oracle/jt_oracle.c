@@ -317,6 +317,16 @@ static void triangle_tangents_fromuv(v3 p1, v3 p2, v3 p3, v2 uv1, v2 uv2, v2 uv3
     }
 }
 
+/* wide records of one binary tree (JT_TRAVERSAL_WIDE, see intersect_scene_wide) */
+typedef struct {
+    float o[3], s[3];
+    int a[3];                          /* N's split axis, then L's and R's (0 for a leaf) */
+    unsigned char lo[3][4], hi[3][4];  /* per axis, per slot */
+    int child[4];                      /* binary node of the slot, -1 empty */
+    int rec[4];                        /* record of an internal child, -1 otherwise */
+} wrec_t;
+typedef struct { int n, cap; wrec_t* r; } wtree_t;
+
 /* ---------------------------------------------------------- scene view */
 typedef struct {
     const jt_scene* scene;
@@ -327,6 +337,8 @@ typedef struct {
     fr3* inst_inverse; /* inverse(frame, true), recomputed per visit by the reference */
     fr3* env_frame;
     fr3* env_inverse;  /* inverse(frame) rigid (src/scene.jl:906) */
+    wtree_t wtlas;     /* JT_TRAVERSAL_WIDE: the TLAS's wide records */
+    wtree_t* wblas;    /* and every BLAS's */
     fr3 camera_frame;
     float camera_aspect; /* cam.aspect, or W/H when --width/--height are given (see setup_ctx) */
     int width, height;
@@ -480,6 +492,229 @@ static scene_isec intersect_instance_bvh(const ctx_t* c, int inst_id, ray3 ray, 
     isec.distance = s.distance;
     isec.hit = 1;
     return isec;
+}
+
+/* ------------------------------------------------- wide traversal (JT_TRAVERSAL_WIDE) */
+/* The build's 4-wide traversal (include/jtrace.h JT_TRAVERSAL_WIDE), restated from
+ * its specification independently of the product's builder (jt_trace.hip build_wide): a record
+ * per internal binary node N (or the root leaf) holding N's grandchildren in slots [LL, LR, RL,
+ * RR] (a leaf child alone in its pair's first slot), their boxes quantised to bytes relative to
+ * N's box, visited near child first in the binary DFS order; every record's children are tested
+ * when the record is visited. Its closest hits equal the binary traversal's up to exact-t ties
+ * and boxes the exact slab test culls by rounding (the quantised boxes are conservative). */
+
+static float w_scale(int e) { /* 2^(e - 127), e a normal float's biased exponent */
+    uint32_t b = (uint32_t)e << 23;
+    float f;
+    memcpy(&f, &b, 4);
+    return f;
+}
+/* the largest lo with o + lo*s <= cmin and the smallest hi with o + hi*s >= cmax, in float */
+static int w_quantize(float o, float s, float cmin, float cmax, unsigned* lo, unsigned* hi) {
+    double f = floor(((double)cmin - (double)o) / (double)s);
+    int q = (int)(f < 0 ? 0 : f > 255 ? 255 : f);
+    while (q > 0 && o + (float)q * s > cmin) q--;
+    while (q < 255 && o + (float)(q + 1) * s <= cmin) q++;
+    if (!(o + (float)q * s <= cmin)) return 0;
+    *lo = (unsigned)q;
+    f = ceil(((double)cmax - (double)o) / (double)s);
+    q = (int)(f < 0 ? 0 : f > 255 ? 255 : f);
+    while (q < 255 && o + (float)q * s < cmax) q++;
+    while (q > 0 && o + (float)(q - 1) * s >= cmax) q--;
+    if (!(o + (float)q * s >= cmax)) return 0;
+    *hi = (unsigned)q;
+    return 1;
+}
+static int w_add(wtree_t* t) {
+    if (t->n == t->cap) {
+        t->cap = t->cap ? 2 * t->cap : 64;
+        t->r = (wrec_t*)realloc(t->r, sizeof(wrec_t) * (size_t)t->cap);
+        if (!t->r) return -1;
+    }
+    return t->n++;
+}
+/* record of binary node `node` (and, recursively, of its internal grandchildren) */
+static int w_build(const jt_bvh_tree* b, int node, wtree_t* t) {
+    int r = w_add(t);
+    if (r < 0) return -1;
+    const jt_bvh_node* N = &b->nodes[node];
+    int slot[4] = {-1, -1, -1, -1}, a1 = 0, a2 = 0;
+    if (!N->internal) {
+        slot[0] = node;
+    } else {
+        const jt_bvh_node* L = &b->nodes[N->start];
+        const jt_bvh_node* R = &b->nodes[N->start + 1];
+        if (L->internal) { slot[0] = L->start; slot[1] = L->start + 1; a1 = L->axis; } else slot[0] = N->start;
+        if (R->internal) { slot[2] = R->start; slot[3] = R->start + 1; a2 = R->axis; } else slot[2] = N->start + 1;
+    }
+    wrec_t w;
+    memset(&w, 0, sizeof w);
+    w.a[0] = N->internal ? N->axis : 0;
+    w.a[1] = a1;
+    w.a[2] = a2;
+    for (int ax = 0; ax < 3; ax++) {
+        double ext = (double)N->bmax[ax] - (double)N->bmin[ax];
+        int e = 1;
+        while (e < 254 && 255.0 * ldexp(1.0, e - 127) < ext) e++;
+        for (;; e++) {
+            if (e > 254) return -1;
+            float sc = w_scale(e);
+            int ok = isfinite(N->bmin[ax] + 255.0f * sc);
+            for (int k = 0; k < 4 && ok; k++) {
+                if (slot[k] < 0) continue;
+                unsigned lo = 0, hi = 0;
+                ok = w_quantize(N->bmin[ax], sc, b->nodes[slot[k]].bmin[ax], b->nodes[slot[k]].bmax[ax], &lo, &hi);
+                w.lo[ax][k] = (unsigned char)lo;
+                w.hi[ax][k] = (unsigned char)hi;
+            }
+            if (ok) break;
+        }
+        w.o[ax] = N->bmin[ax];
+        w.s[ax] = w_scale(e);
+    }
+    for (int k = 0; k < 4; k++) {
+        w.child[k] = slot[k];
+        w.rec[k] = -1;
+    }
+    t->r[r] = w;
+    for (int k = 0; k < 4; k++) {
+        if (slot[k] < 0 || !b->nodes[slot[k]].internal) continue;
+        int cr = w_build(b, slot[k], t);
+        if (cr < 0) return -1;
+        t->r[r].rec[k] = cr;
+    }
+    return r;
+}
+/* visit order of the slots (binary near-first DFS): the pair of N's near child first, in a pair
+ * its near child first; dsign = ray_dsign with the near flip (1: start is the near child) */
+static void w_order(const wrec_t* w, const int* dsign, int* order) {
+    int p0 = dsign[w->a[0]] ? 0 : 1;
+    for (int q = 0; q < 2; q++) {
+        int p = q == 0 ? p0 : 1 - p0;
+        int f = dsign[w->a[1 + p]] ? 0 : 1;
+        order[2 * q] = 2 * p + f;
+        order[2 * q + 1] = 2 * p + 1 - f;
+    }
+}
+static void w_test(const wrec_t* w, const ray3* ray, v3 dinv, int* hit) {
+    for (int k = 0; k < 4; k++) {
+        hit[k] = 0;
+        if (w->child[k] < 0) continue;
+        float bmin[3], bmax[3];
+        for (int ax = 0; ax < 3; ax++) {
+            bmin[ax] = w->o[ax] + (float)w->lo[ax][k] * w->s[ax];
+            bmax[ax] = w->o[ax] + (float)w->hi[ax][k] * w->s[ax];
+        }
+        hit[k] = intersect_bbox(ray, dinv, bmin, bmax);
+    }
+}
+static void w_shape(const ctx_t* c, int shape_id, int r, ray3* ray, v3 dinv, const int* dsign, shape_isec* isec,
+                    scratch_t* sc) {
+    const jt_bvh_tree* bvh = &c->bvh->blas[shape_id];
+    const jt_shape* shape = &c->scene->shapes[shape_id];
+    const wrec_t* w = &c->wblas[shape_id].r[r];
+    sc->cnt.nodes++;
+    int hit[4], order[4];
+    w_test(w, ray, dinv, hit);
+    w_order(w, dsign, order);
+    for (int q = 0; q < 4; q++) {
+        int k = order[q];
+        if (!hit[k]) continue;
+        const jt_bvh_node* node = &bvh->nodes[w->child[k]];
+        if (node->internal) {
+            w_shape(c, shape_id, w->rec[k], ray, dinv, dsign, isec, sc);
+            continue;
+        }
+        for (int i = node->start; i < node->start + node->num; i++) {
+            int e = bvh->primitives[i];
+            prim_isec p;
+            sc->cnt.prims++;
+            if (shape->ntriangles > 0) {
+                const int32_t* t3 = &shape->triangles[3 * e];
+                p = intersect_triangle(ray, pos3(shape, t3[0]), pos3(shape, t3[1]), pos3(shape, t3[2]));
+            } else {
+                const int32_t* q4 = &shape->quads[4 * e];
+                p = intersect_quad(ray, pos3(shape, q4[0]), pos3(shape, q4[1]), pos3(shape, q4[2]), pos3(shape, q4[3]));
+            }
+            if (!p.hit) continue;
+            isec->element = e;
+            isec->uv = p.uv;
+            isec->distance = p.distance;
+            isec->hit = 1;
+            ray->tmax = p.distance;
+        }
+    }
+}
+/* intersect_shape_bvh on the wide records */
+static shape_isec intersect_shape_wide(const ctx_t* c, int shape_id, ray3 ray, scratch_t* sc) {
+    shape_isec isec = {-1, {0, 0}, 0, 0};
+    v3 dinv = V3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+    int dsign[3] = {(ray.d.x < 0) ^ 1, (ray.d.y < 0) ^ 1, (ray.d.z < 0) ^ 1};
+    w_shape(c, shape_id, 0, &ray, dinv, dsign, &isec, sc);
+    return isec;
+}
+static void w_scene(const ctx_t* c, int r, ray3* ray, v3 dinv, const int* dsign, scene_isec* isec, scratch_t* sc) {
+    const jt_bvh_tree* bvh = &c->bvh->tlas;
+    const wrec_t* w = &c->wtlas.r[r];
+    sc->cnt.nodes++;
+    int hit[4], order[4];
+    w_test(w, ray, dinv, hit);
+    w_order(w, dsign, order);
+    for (int q = 0; q < 4; q++) {
+        int k = order[q];
+        if (!hit[k]) continue;
+        const jt_bvh_node* node = &bvh->nodes[w->child[k]];
+        if (node->internal) {
+            w_scene(c, w->rec[k], ray, dinv, dsign, isec, sc);
+            continue;
+        }
+        for (int i = node->start; i < node->start + node->num; i++) {
+            int inst_id = bvh->primitives[i];
+            sc->cnt.instances++;
+            ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], ray);
+            shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc);
+            if (!s.hit) continue;
+            isec->instance = inst_id;
+            isec->element = s.element;
+            isec->uv = s.uv;
+            isec->distance = s.distance;
+            isec->hit = 1;
+            ray->tmax = s.distance;
+        }
+    }
+}
+/* intersect_scene_bvh on the wide records */
+static scene_isec intersect_scene_wide(const ctx_t* c, ray3 ray, scratch_t* sc) {
+    scene_isec isec = {-1, -1, {0, 0}, 0, 0};
+    sc->cnt.rays++;
+    if (c->bvh->tlas.nnodes == 0) return isec;
+    v3 dinv = V3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+    int dsign[3] = {(ray.d.x < 0) ^ 1, (ray.d.y < 0) ^ 1, (ray.d.z < 0) ^ 1};
+    w_scene(c, 0, &ray, dinv, dsign, &isec, sc);
+    return isec;
+}
+/* intersect_instance_bvh on the wide records */
+static scene_isec intersect_instance_wide(const ctx_t* c, int inst_id, ray3 ray, scratch_t* sc) {
+    scene_isec isec = {-1, -1, {0, 0}, 0, 0};
+    sc->cnt.light_queries++;
+    sc->cnt.instances++;
+    ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], &ray);
+    shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc);
+    if (!s.hit) return isec;
+    isec.instance = inst_id;
+    isec.element = s.element;
+    isec.uv = s.uv;
+    isec.distance = s.distance;
+    isec.hit = 1;
+    return isec;
+}
+/* the traversal jt_params.traversal selects */
+static scene_isec scene_query(const ctx_t* c, ray3 ray, scratch_t* sc) {
+    return c->params->traversal == JT_TRAVERSAL_WIDE ? intersect_scene_wide(c, ray, sc) : intersect_scene_bvh(c, ray, sc);
+}
+static scene_isec instance_query(const ctx_t* c, int inst_id, ray3 ray, scratch_t* sc) {
+    return c->params->traversal == JT_TRAVERSAL_WIDE ? intersect_instance_wide(c, inst_id, ray, sc)
+                                                     : intersect_instance_bvh(c, inst_id, ray, sc);
 }
 
 /* --------------------------------------------------------------- scene.jl evaluation */
@@ -1251,7 +1486,7 @@ static float sample_lights_pdf(const ctx_t* c, v3 position, v3 direction, scratc
             float lpdf = 0.0f;
             v3 next_position = position;
             for (int bounce = 0; bounce < 100; bounce++) {
-                scene_isec isec = intersect_instance_bvh(c, light->instance, make_ray(next_position, direction), sc);
+                scene_isec isec = instance_query(c, light->instance, make_ray(next_position, direction), sc);
                 if (!isec.hit) break;
                 v3 lposition = eval_position(c, light->instance, isec.element, isec.uv);
                 v3 lnormal = eval_element_normal(c, light->instance, isec.element);
@@ -1307,7 +1542,7 @@ static path_result trace_path(const ctx_t* c, ray3 ray, rng_t* rng, scratch_t* s
     int bounce = -1;
     while (bounce < params->bounces) {
         bounce += 1;
-        scene_isec isec = intersect_scene_bvh(c, ray, sc);
+        scene_isec isec = scene_query(c, ray, sc);
         if (sc->overflow) break;
         if (!isec.hit) {
             if (bounce > 0 || !params->envhidden) radiance = add3(radiance, mul3(weight, eval_environment(c, ray.d)));
@@ -1423,7 +1658,7 @@ static path_result trace_naive(const ctx_t* c, ray3 ray, rng_t* rng, scratch_t* 
     int bounce = -1;
     while (bounce < params->bounces) {
         bounce += 1;
-        scene_isec isec = intersect_scene_bvh(c, ray, sc);
+        scene_isec isec = scene_query(c, ray, sc);
         if (sc->overflow) break;
         if (!isec.hit) {
             if (bounce > 0 || !params->envhidden) radiance = add3(radiance, mul3(weight, eval_environment(c, ray.d)));
@@ -1613,6 +1848,15 @@ static int setup_ctx(ctx_t* c, const jt_scene* scene, const jt_scene_bvh* bvh, c
         c->env_frame[k] = frame_from(scene->environments[k].frame);
         c->env_inverse[k] = inverse_frame(&c->env_frame[k], 0);
     }
+    if (params->traversal == JT_TRAVERSAL_WIDE) {
+        c->wblas = (wtree_t*)calloc((size_t)scene->nshapes + 1, sizeof(wtree_t));
+        if (!c->wblas) return JT_ERR_NOMEM;
+        if (bvh->tlas.nnodes > 0 && w_build(&bvh->tlas, 0, &c->wtlas) < 0) return JT_ERR_UNSUPPORTED;
+        for (int s = 0; s < scene->nshapes; s++)
+            if (bvh->blas[s].nnodes > 0 && w_build(&bvh->blas[s], 0, &c->wblas[s]) < 0) return JT_ERR_UNSUPPORTED;
+    } else if (params->traversal != JT_TRAVERSAL_REFERENCE && params->traversal != JT_TRAVERSAL_NEAR) {
+        return JT_ERR_INVALID;
+    }
     return JT_OK;
 }
 static void free_ctx(ctx_t* c) {
@@ -1620,6 +1864,10 @@ static void free_ctx(ctx_t* c) {
     free(c->inst_inverse);
     free(c->env_frame);
     free(c->env_inverse);
+    free(c->wtlas.r);
+    if (c->wblas)
+        for (int s = 0; s < c->scene->nshapes; s++) free(c->wblas[s].r);
+    free(c->wblas);
 }
 
 int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights, const jt_params* params,

@@ -81,7 +81,7 @@ def source_hash(root=ROOT):
 
 CUS = 256
 XCDS = 8
-KERNEL_RE = re.compile(r"(trace_kernel\w*<\d+, \d+, (?:true|false), 0, \d+>)")
+KERNEL_RE = re.compile(r"(trace_kernel\w*<\d+, \d+, (?:true|false), 0, \d+, (?:true|false)>)")  # <.., WIDE>
 
 
 def timed_kernel(stats_csv):
@@ -137,6 +137,29 @@ def derive(rec):
         if "lane_util" in out and pmc.get("SQ_INSTS_VALU"):
             out["valu_lane_ops"] = pmc["SQ_INSTS_VALU"] * 64.0 * out["lane_util"]
             out["valu_peak_gops"] = CUS * 4 * 0.5 * 64 * clk / 1e9
+        gui = pmc["GRBM_GUI_ACTIVE"] / XCDS  # clock cycles of the launch
+        if pmc.get("TA_TA_BUSY_sum"):
+            out["ta_busy_frac"] = pmc["TA_TA_BUSY_sum"] / CUS / gui
+        if pmc.get("TD_TC_STALL_sum") and pmc.get("TD_TD_BUSY_sum"):
+            out["td_tc_stall_frac_of_busy"] = pmc["TD_TC_STALL_sum"] / pmc["TD_TD_BUSY_sum"]
+        if pmc.get("TCC_HIT_sum") is not None and pmc.get("TCC_MISS_sum") is not None and \
+                pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"] > 0:
+            out["l2_hit_rate"] = pmc["TCC_HIT_sum"] / (pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"])
+            out["l2_requests_per_launch"] = pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"]
+        if pmc.get("TCP_TOTAL_CACHE_ACCESSES_sum") and pmc.get("SQ_INSTS_VMEM_RD"):
+            # L1 (TCP) cache accesses per vector-memory read wave-instruction (a divergent gather
+            # touches one line per distinct address)
+            out["l1_accesses_per_vmem_rd"] = pmc["TCP_TOTAL_CACHE_ACCESSES_sum"] / pmc["SQ_INSTS_VMEM_RD"]
+        if pmc.get("TCP_PENDING_STALL_CYCLES_sum"):
+            out["tcp_pending_stall_frac"] = pmc["TCP_PENDING_STALL_CYCLES_sum"] / CUS / gui
+        if pmc.get("SQ_WAVE_CYCLES"):
+            # where a resident wave's cycles go (disjoint, MI355X_MICROARCH.md rocprofv3 PMC slots):
+            # issuing, parked on s_waitcnt / barrier (memory latency), or ready but not issued
+            for k, name in (("SQ_ACTIVE_INST_ANY", "wave_active_frac"), ("SQ_WAIT_ANY", "wave_wait_frac"),
+                            ("SQ_WAIT_INST_ANY", "wave_issue_stall_frac"), ("SQ_WAIT_INST_LDS", "wave_lds_stall_frac"),
+                            ("SQ_ACTIVE_INST_SCA", "wave_salu_frac"), ("SQ_ACTIVE_INST_LDS", "wave_lds_frac")):
+                if pmc.get(k) is not None:
+                    out[name] = pmc[k] / pmc["SQ_WAVE_CYCLES"]
         if pmc.get("SQ_INSTS_VMEM_RD"):
             out["vmem_rd_per_launch"] = pmc["SQ_INSTS_VMEM_RD"]
             out["vmem_rd_gips"] = pmc["SQ_INSTS_VMEM_RD"] / pd / 1e9

@@ -11,10 +11,10 @@ tests/test_gpu_parity.py: >= 99.9 % of pixels within 1e-3 relative on every chan
 image mean within 1e-4 relative, hit counts identical; over the whole frame, the closest-hit ray
 and light-query counts within 0.1 % + 8.
 
-Every frame is checked in both BVH child orders: near-first (DEFAULT_TRAVERSAL, the order bench.py
-times) and the reference's far-first order (src/bvh.jl:331-341); the oracle restates both. The
-fraction of pixels whose near-order value differs from the reference-order value at all (exact-t
-ties only) is printed per frame.
+Every frame is checked in each traversal: the binary near-first order (DEFAULT_TRAVERSAL), its
+4-wide quantised-record form (wide) and the reference's far-first order (src/bvh.jl:331-341); the
+oracle restates all three. The fraction of pixels whose value differs between two traversals at
+all (exact-t ties only) is printed per frame.
 """
 import numpy as np
 import pytest
@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 
 # scene: (width, height, row bands)
 FRAMES = {"features2": (1920, 1080, 1), "bathroom1": (1920, 1080, 2), "ecosys": (3840, 1920, 4)}
-ORDERS = ["near", "reference"]
+ORDERS = ["near", "wide", "reference"]
 _gpu = {}
 _oracle_counts = {}
 
@@ -42,11 +42,11 @@ def gpu_frame(lib, abi, name, order):
         st.trace_range(0, 1)
         _gpu[(name, order)] = (p, st.get_image(), *st.get_aovs(), st.counters(), st.describe())
         st.close()
-        other = [k for k in _gpu if k[0] == name and k[1] != order]
-        if other:
-            a, b = _gpu[(name, "near")][1], _gpu[(name, "reference")][1]
-            print(f"{name} {W}x{H}x1: pixels differing between the near and reference orders "
-                  f"{float(np.mean(np.any(a != b, axis=-1))):.3e}")
+        for other in ORDERS:
+            if other != order and (name, other) in _gpu:
+                a, b = _gpu[(name, order)][1], _gpu[(name, other)][1]
+                print(f"{name} {W}x{H}x1: pixels differing between the {order} and {other} traversals "
+                      f"{float(np.mean(np.any(a != b, axis=-1))):.3e}")
     return _gpu[(name, order)]
 
 

@@ -278,9 +278,10 @@ def _full_parity(abi, lib, oracle, scene_abi, params, spp, label):
         assert compare_images(a, b)["frac_pix_rel_le_1e-3"] >= 0.999
 
 
-# "near" is the order bench.py times (DEFAULT_TRAVERSAL); "reference" is the reference's own
-# far-first order (src/bvh.jl:331-341). Both are restated by the oracle.
-ORDERS = ["near", "reference"]
+# "near" is the binary near-first order (DEFAULT_TRAVERSAL), "wide" its 4-wide quantised-record
+# form (JT_TRAVERSAL_WIDE), "reference" the reference's own far-first order (src/bvh.jl:331-341).
+# All three are restated by the oracle.
+ORDERS = ["near", "wide", "reference"]
 
 
 @pytest.mark.parametrize("order", ORDERS)

@@ -18,7 +18,7 @@ from test_gpu_scenes import check_parity, render_gpu, render_oracle, scene_abi
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("order", ["near", "reference"])
+@pytest.mark.parametrize("order", ["near", "wide", "reference"])
 @pytest.mark.parametrize("sampler", [1, 2])
 @pytest.mark.parametrize("name,lds", [("cornellbox", "lds"), ("cornellbox", "hbm"), ("features1", None),
                                       ("features2", None), ("bathroom1", None), ("ecosys", None)])
@@ -48,21 +48,23 @@ def test_abi_zero_value_is_reference_order(gpu, abi, lib, oracle, cornell_abi):
     check_parity(g, o, "cornellbox/zero-value/reference")
 
 
+@pytest.mark.parametrize("order", ["near", "wide"])
 @pytest.mark.parametrize("name", ["cornellbox", "features2", "bathroom1", "ecosys"])
-def test_near_vs_reference_order(gpu, abi, lib, cornell_abi, name):
-    """Near-first against the reference order on the GPU: the §8(c) bar holds between the two
-    images, hit counts agree to ties, and fewer nodes are popped per closest-hit query."""
+def test_order_vs_reference_order(gpu, abi, lib, cornell_abi, name, order):
+    """Near-first (binary or wide) against the reference order on the GPU: the §8(c) bar holds
+    between the two images, hit counts agree to ties, and fewer nodes are visited per closest-hit
+    query (a wide record visit counts as one node)."""
     sa = cornell_abi if name == "cornellbox" else scene_abi(name)
     out = {}
-    for order in ("reference", "near"):
-        p = make_params(abi, resolution=160, samples=4, traversal=order)
-        out[order] = render_gpu(lib, sa, p, 0, 4)
-    r, n = out["reference"], out["near"]
+    for o in ("reference", order):
+        p = make_params(abi, resolution=160, samples=4, traversal=o)
+        out[o] = render_gpu(lib, sa, p, 0, 4)
+    r, n = out["reference"], out[order]
     stats = compare_images(n[0], r[0])
     differ = float(np.mean(np.any(n[0] != r[0], axis=-1)))
     nodes_r = r[4]["nodes"] / r[4]["rays"]
     nodes_n = n[4]["nodes"] / n[4]["rays"]
-    print(f"{name}: pixels differing from the reference order {differ:.6f}, {stats}; "
+    print(f"{name} {order}: pixels differing from the reference order {differ:.6f}, {stats}; "
           f"nodes/ray {nodes_r:.2f} -> {nodes_n:.2f}, prims/ray {r[4]['prims'] / r[4]['rays']:.2f} -> "
           f"{n[4]['prims'] / n[4]['rays']:.2f}")
     assert stats["frac_pix_rel_le_1e-3"] >= 0.999, stats

@@ -48,6 +48,15 @@ def test_two_rank_shards_equal_single_render(abi, oracle, cornell_abi, tmp_path)
     single = oracle.trace(cornell_abi, oracle.build_bvh(cornell_abi), oracle.make_lights(cornell_abi), p, RES, RES,
                           0, SPP)[0]
     np.testing.assert_allclose(combined, single, rtol=1e-5, atol=1e-6)
+    # the bench's reduced-image check (jtrace/parallel.py) accepts the reduce and rejects a
+    # missing shard or a wrong weight
+    from jtrace.parallel import compare_signature, image_signature
+    ref = image_signature(single, block=8)
+    assert compare_signature(image_signature(combined, block=8), ref)["ok"]
+    half = oracle.trace(cornell_abi, oracle.build_bvh(cornell_abi), oracle.make_lights(cornell_abi), p, RES, RES,
+                        0, SPP // 2)[0]
+    assert not compare_signature(image_signature(half * 0.5, block=8), ref)["ok"]  # one shard, weight n_r / S
+    assert not compare_signature(image_signature(combined * 1.01, block=8), ref)["ok"]
 
 
 def test_shard_ranges_cover_all_samples():

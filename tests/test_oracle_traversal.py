@@ -20,6 +20,26 @@ def test_oracle_near_order_matches_reference_order(abi, oracle, cornell_abi):
     assert n[4]["nodes"] < r[4]["nodes"], (n[4]["nodes"], r[4]["nodes"])
 
 
+def test_oracle_wide_matches_binary_orders(abi, oracle, cornell_abi):
+    """The wide traversal (JT_TRAVERSAL_WIDE: 4-wide records with conservative quantised boxes)
+    finds the same closest hits as the binary near-first order up to exact-t ties, visits fewer
+    nodes (one record visit tests up to four boxes), and tests at least as many primitives
+    (quantised boxes are never tighter)."""
+    ob = oracle.build_bvh(cornell_abi)
+    ol = oracle.make_lights(cornell_abi)
+    out = {}
+    for order in ("near", "wide"):
+        p = make_params(abi, resolution=64, samples=2, traversal=order)
+        out[order] = oracle.trace(cornell_abi, ob, ol, p, 64, 64, 0, 2)
+    n, w = out["near"], out["wide"]
+    stats = compare_images(w[0], n[0])
+    assert stats["frac_pix_rel_le_1e-3"] >= 0.999, stats
+    assert np.array_equal(w[3], n[3])
+    assert w[4]["rays"] == n[4]["rays"] and w[4]["light_queries"] == n[4]["light_queries"]
+    assert w[4]["nodes"] < n[4]["nodes"], (w[4]["nodes"], n[4]["nodes"])
+    assert w[4]["prims"] >= n[4]["prims"]
+
+
 def test_params_carry_the_traversal_order(abi):
     from jtrace.cli import DEFAULT_TRAVERSAL, Params, parse_cli_args
     # one default for the parser, the dataclass and make_params: near first (the benched order)
@@ -28,5 +48,6 @@ def test_params_carry_the_traversal_order(abi):
     assert make_params(abi).traversal == 1
     assert make_params(abi, traversal="near").traversal == 1
     assert make_params(abi, traversal="reference").traversal == 0
+    assert make_params(abi, traversal="wide").traversal == 2
     assert abi.jt_params().traversal == 0  # the C-ABI zero value is the reference's order
     assert abi.jt_params.traversal.offset == 64 and abi.C.sizeof(abi.jt_params) == 72
