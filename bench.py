@@ -115,6 +115,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-spp", type=int, default=128)
+    ap.add_argument("--tile-groups", type=int, default=0,
+                    help="N > 1: split the tiles into G interleaved groups x N/G sample ranges (0: automatic)")
+    ap.add_argument("--as-rank-of", type=int, default=0,
+                    help="N=1: trace rank 0's share of an N-rank run (per-GPU rate and roofline of that share)")
     ap.add_argument("--write-signature", action="store_true",
                     help="N=1: record this workload's image fingerprint in profiles/image_signatures.json")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
@@ -167,8 +171,18 @@ def main():
             "total_s": round(t_create - t_0, 3)}
     W, H, S = state.width, state.height, args.spp
     from jtrace.parallel import (compare_signature, image_signature, load_signature, reduce_running_means,
-                                 save_signature, shard_range)
-    s0, s1 = shard_range(S, world, rank)
+                                 save_signature, split_plan)
+    # this rank's share: 1/G of the 8x8 tiles (G = --tile-groups) x a contiguous
+    # 1/(N/G) of the samples; G = 1 is the pure sample split
+    groups = args.tile_groups if args.tile_groups > 0 else 1
+    # --as-rank-of N (N=1 runs only): trace rank 0's share of an N-rank run, to measure it on one GPU
+    plan_world, plan_rank = (args.as_rank_of, 0) if (args.as_rank_of and world == 1) else (world, rank)
+    share, s0, s1 = split_plan(plan_world, plan_rank, S, groups)
+    if share is not None:  # the context must be created with the option: recreate it
+        state.close()
+        abi.set_option(lib, "tile_share", share)
+        state = trace.make_trace_state(sa, bvh, lights, jp, lib)
+        abi.set_option(lib, "tile_share", None)
 
     img_t = None
     if world > 1:
@@ -233,7 +247,10 @@ def main():
     # N > 1 — against the one-GPU signature committed for this workload (profiles/image_signatures.json,
     # jtrace/parallel.py): a wrong shard split, weight or reduce fails the run loudly
     image_check = None
-    if rank == 0:
+    partial = world == 1 and plan_world > 1  # --as-rank-of: one rank's share only, not the image
+    if rank == 0 and partial:
+        image_check = {"ok": None, "why": f"--as-rank-of {plan_world}: rank 0's share only"}
+    elif rank == 0:
         img_final = (reduced[0].detach().cpu().numpy().reshape(H, W, 4) if world > 1 else state.get_image())
         sig = image_signature(img_final)
         sig_key = f"{Path(args.scene).stem} {args.sampler} {W}x{H}x{S}spp traversal={args.traversal}" + \
@@ -254,7 +271,7 @@ def main():
     # and the fraction of pixels whose final running mean differs from the near-first image (only
     # exact-t ties can resolve differently)
     ref_order = None
-    if rank == 0 and world == 1 and args.traversal != "reference" and not args.no_reference_order:
+    if rank == 0 and world == 1 and not partial and args.traversal != "reference" and not args.no_reference_order:
         img_near = state.get_image()
         rp = abi.make_params(Params(scene=args.scene, samples=args.spp, sampler=2 if args.sampler == "naive" else 1,
                                     width=args.width, height=args.height, device=dev, batch=args.spp,
@@ -289,7 +306,7 @@ def main():
     # workload; the GPU then re-traces exactly those samples so the two ray counts — hence the
     # two cameras and framings — are checked to agree (a libm ulp may flip a rare path: <= 0.1 %)
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline and world == 1:
+    if rank == 0 and not args.no_cpu_baseline and world == 1 and not partial:
         cpu = cpu_baseline(sa, jp, W, H, args.cpu_threads, args.cpu_spp, args.highqualitybvh)
         state.reset()
         state.trace_range(0, args.cpu_spp)
@@ -311,6 +328,7 @@ def main():
         logical = algorithmic_bytes(per_launch, shade_record_bytes(scene),
                                     any(len(s.quads) for s in scene.shapes), args.traversal == "wide")
         workload = f"{name} {args.sampler} {W}x{H} {s1 - s0} samples/launch" + \
+            (f" tiles 1/{groups}" if groups > 1 else "") + \
             ("" if args.traversal == "reference" else f" traversal={args.traversal}") + \
             (" bvh=sah" if args.highqualitybvh else "")
         sys.path.insert(0, str(ROOT / "scripts"))
@@ -368,11 +386,13 @@ def main():
             "data": f"scene: the reference's own {name} (assets/scenes/{name}), seed 0x5EED"
                     + (f"; {'; '.join(scene.notes)}" if scene.notes else ""),
             "config": {"workload": f"{name} {args.sampler} {W}x{H}x{S}spp", "scene": name,
+                       "split": {"tile_groups": groups, "sample_ranges": world // groups,
+                                 "rank0_share": {"tiles": share or "all", "samples": [s0, s1]}},
                        "sampler": args.sampler, "width": W, "height": H, "spp": S, "bounces": 8,
                        "traversal": args.traversal, "bvh": "sah" if args.highqualitybvh else "middle",
-                       "parallelism": f"sample-range shards x{world} + RCCL reduce"},
+                       "parallelism": f"{groups} tile groups x {world // groups} sample ranges + RCCL reduce"},
             "render_s": round(ms_per_step / 1e3, 4),
-            "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 2),
+            "msamples_per_s": round((agg["paths"] if partial else W * H * S * args.steps) / elapsed / 1e6, 2),
             "mlight_queries_per_s": round(agg["light_queries"] * world / elapsed / 1e6, 2),
             "time_to_first_pixel_s": ttfp,
             "options": dict(o.partition("=")[::2] for o in args.opt) or None,

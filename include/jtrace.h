@@ -275,11 +275,12 @@ int jt_device_count(int32_t* out);
  *   "chunk", "chunk_min"     samples per work unit; the halving tail of the chunk table
  *   "wait_lanes", "light_lanes"  the shading gate; the light-hit step gate
  *   "multi_split" "tiles"|"samples"  jt_create_multi's split mode
- * Test-only (they change WHAT is traced, for tests that reproduce a multi-device share or the
- * stack overflow path on one GPU; jt_describe reports them when set):
- *   "test_tiles" "k,o"       trace only the 8x8 tiles o, o + k, o + 2k, ... (one device's share of
- *                            a k-device tile split); ignored by jt_create_multi's sample split
- *   "test_lds_ring" "1|2|4|8|16"  use that many LDS ring entries (the rest overflow to HBM) */
+ * Options that change WHAT a context traces (jt_describe reports them when set):
+ *   "tile_share" "k,o"       trace only the 8x8 tiles o, o + k, o + 2k, ...: this process's share
+ *                            of a k-way tile split when one process per GPU shards a render by
+ *                            tiles (bench.py); jt_create_multi sets its own split instead
+ *   "test_lds_ring" "1|2|4|8|16"  (tests only) use that many LDS ring entries, the rest overflow to
+ *                            HBM: the overflow path on small scenes */
 int jt_set_option(const char* name, const char* value);
 
 /* ---- host helpers (CPU only) ------------------------------------------------------- */

@@ -1304,7 +1304,8 @@ struct DAccum {
                                    // [7]: tile-order wait timeouts (must stay 0)
     unsigned* work;                // unit counters of the launch, one per XCD band at work[16 b]
                                    // (zeroed before each launch)
-    int* tile_done;                // per 8x8 tile: sample chunks accumulated in this launch
+    int* tile_done;                // chunks accumulated in this launch: per 8x8 tile (trace_body) or per
+                                   // pixel slot tile * 64 + l (trace_body_items)
 };
 
 // Work units: (sample chunk c, 8x8 pixel tile t), fetched by whole waves from atomic counters,
@@ -1721,6 +1722,330 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     }
 }
 
+// ============================================================================ per-lane work items
+// JT_LANE_ITEMS: the work units stay (8x8 tile t, sample chunk c), fetched by whole waves, but a
+// lane is no longer tied to its wave's unit: a lane that has finished its pixel's chunk takes the
+// next pixel of its wave's current unit at once, and the wave fetches the next unit when every
+// pixel of the current one has been handed out. A wave therefore never waits for the slowest
+// lane of a unit (the "dead lanes" of DESIGN.md §2); lanes hold pixels of at most a few
+// consecutive units, so neighbouring lanes stay spatially close. The wave-level hand-out is a
+// ballot and a prefix count (mbcnt): lane k of the needy lanes takes pixel bnext + k.
+// A pixel's chunks still run in order (the running mean is order-dependent, src/trace.jl:631-648):
+// a lane that takes (c, pixel) with c > 0 starts once (c - 1, pixel) is published, which is by
+// then almost always the case (units are numbered chunk-major). The hand-off of one pixel's
+// running means between lanes — possibly on another CU or XCD — is write-through: the finishing
+// lane stores them with sc1 stores (agent-scope relaxed atomics, 8 B each), the wave drains its
+// stores (s_waitcnt vmcnt(0)), then the lane stores the pixel's done word; the taking lane polls
+// that word (relaxed agent load) and reads the means with sc1 loads, so no cache-wide fence is
+// needed (cdna_hip_programming.md Guideline 16, write-through hand-off). A lane whose pixel is not
+// ready yet does not spin: it is re-checked every iteration while the other lanes work.
+// Results are bit-identical: every pixel's samples run in order with the same float operations.
+#ifndef JT_LANE_ITEMS
+#define JT_LANE_ITEMS 1
+#endif
+#ifndef JT_ITEM_FIRST_POP
+#define JT_ITEM_FIRST_POP 1
+#endif
+// a lane's item: bits 0-25 the pixel's slot tile * 64 + l (l: pixel of the 8x8 tile; jt_create
+// keeps tiles below 2^20), 26-30 its chunk, 31 ITEM_BLOCKED (taken, waiting for the previous
+// chunk of the pixel); ITEM_NONE: no pixel
+constexpr unsigned ITEM_NONE = 0xffffffffu, ITEM_BLOCKED = 0x80000000u, ITEM_SLOT_MASK = (1u << 26) - 1u;
+constexpr int ITEM_CHUNK_SHIFT = 26;
+__device__ __forceinline__ int item_chunk(unsigned item) { return (int)((item >> ITEM_CHUNK_SHIFT) & 31u); }
+__device__ __forceinline__ unsigned long long ld_sc1(const void* p) {
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(void* p, unsigned long long v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long pack2(float a, float b) {
+    return (unsigned long long)__float_as_uint(a) | (unsigned long long)__float_as_uint(b) << 32;
+}
+__device__ __forceinline__ float lo_f(unsigned long long v) { return __uint_as_float((unsigned)v); }
+__device__ __forceinline__ float hi_f(unsigned long long v) { return __uint_as_float((unsigned)(v >> 32)); }
+
+template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, bool WIDE>
+__device__ __forceinline__ void trace_body_items(const DScene& S, const DParams& P, int s_begin, int s_end,
+                                                 const DAccum& A, int* stack) {
+    static_assert(lane_lds(F), "the per-lane item body keeps the lane's sample index in LDS");
+    const int lane = threadIdx.x & 63;
+    if constexpr ((F & (FT_TEX | FT_ENV)) != 0) {  // the texel-decode LUTs into LDS (tex_lut)
+        for (int k = threadIdx.x; k < 512; k += BLOCK) tex_lut[k] = k < 256 ? S.srgb_lut[k] : S.byte_lut[k - 256];
+    }
+    // chunk boundaries in LDS: a lane's chunk is per lane here, so its end is looked up per lane
+    __shared__ int cb_lds[JT_MAX_CHUNKS + 2];
+    for (int k = threadIdx.x; k < JT_MAX_CHUNKS + 2; k += BLOCK) {
+        int a, b;
+        if (k < num_chunks(P, s_begin, s_end)) chunk_range(P, s_begin, s_end, k, a, b);
+        else a = b = s_end;
+        cb_lds[k] = b;  // end of chunk k
+    }
+    __syncthreads();
+    Counters cnt{0, 0, 0, 0};
+    constexpr bool WC = !ft_none(F);
+    unsigned w_paths = 0, w_rays = 0, w_lq = 0;
+    __shared__ unsigned wave_cnt[WC ? 1 : (BLOCK / 64) * 4];
+    unsigned* const wcnt = wave_cnt + (WC ? 0 : (threadIdx.x >> 6) * 4);
+    if (!WC && lane < 3) wcnt[lane] = 0u;
+    auto lds_count = [&](int k, bool c) {
+        if (c) __hip_atomic_fetch_add(wcnt + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    __shared__ float acc_lds[acc_slots(F) * BLOCK];
+    float* acc = acc_lds + threadIdx.x;
+    int* const acc_i = reinterpret_cast<int*>(acc);
+    const int tiles_x = (P.width + 7) / 8, tiles = launch_tiles(P);
+    const int nchunks = num_chunks(P, s_begin, s_end);
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    int band_k = 0;
+    int ut = 0, uc = 0, bnext = 64;  // the wave's current unit (tile, chunk) and its next pixel to hand out
+    bool drained = false;            // every band's units handed out
+    unsigned item = ITEM_NONE;       // the lane's pixel (ITEM_* above)
+    int spins = 0;                   // iterations in which every held pixel waited (bounded)
+    bool next_sample = false;        // the lane's next sample starts at the top of the iteration
+    int pixel = 0;                   // its image index (RNG key, HBM stack overflow area)
+    Aov aov{acc, 0.0f, P.first};
+    Path st;
+    st.pk = acc + acc_base_slots(F) * BLOCK;
+    Trav T;
+    T.sp = -1;
+    T.nprim = 0;
+    T.nxt = W_EMPTY;
+    for (;;) {
+        // ---- hand out pixels to the lanes without one (wave-uniform control)
+        for (;;) {
+            const unsigned long long needm = __builtin_amdgcn_ballot_w64(item == ITEM_NONE);
+            if (!needm || drained) break;
+            if (bnext >= 64) {  // the next unit of this XCD's band, or of the next band
+                const int band = (int)((xcc + (unsigned)band_k) & (NBANDS - 1));
+                const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
+                unsigned unit = 0;
+                if (lane == 0) unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
+                unit = __builtin_amdgcn_readfirstlane(unit);
+                if (unit >= (unsigned)bn * (unsigned)nchunks) {
+                    if (++band_k >= NBANDS) drained = true;
+                    continue;
+                }
+                uc = (int)(unit / (unsigned)bn);
+                ut = (bt0 + (int)(unit % (unsigned)bn)) * P.tile_stride + P.tile_offset;
+                bnext = 0;
+            }
+            const int nneed = lane_count(needm), take = nneed < 64 - bnext ? nneed : 64 - bnext;
+            const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(needm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)needm, 0u));
+            if (item == ITEM_NONE && rank < take) {
+                const int l = bnext + rank;
+                const int i = (ut % tiles_x) * 8 + (l & 7), j = (ut / tiles_x) * 8 + (l >> 3);
+                // a pixel outside the image (edge tiles) is skipped: the lane takes another
+                if (i < P.width && j < P.height) {
+                    item = (unsigned)(ut * 64 + l) | (unsigned)uc << ITEM_CHUNK_SHIFT | ITEM_BLOCKED;
+                    pixel = j * P.width + i;
+                }
+            }
+            bnext += take;
+        }
+        // ---- lanes whose pixel's previous chunk is published take it: running means from HBM
+        // (sc1 loads), the chunk's first sample
+        bool start = next_sample;
+        if (item != ITEM_NONE && (item & ITEM_BLOCKED)) {
+            const int c = item_chunk(item);
+            if (c == 0 || spins > (1 << 22) ||
+                __hip_atomic_load(A.tile_done + (item & ITEM_SLOT_MASK), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c) {
+                start = true;
+                item &= ~ITEM_BLOCKED;
+                const unsigned long long i0 = ld_sc1(&A.image[pixel].x), i1 = ld_sc1(&A.image[pixel].z);
+                const unsigned long long a0 = ld_sc1(&A.albedo[pixel].x), a1 = ld_sc1(&A.albedo[pixel].z);
+                const unsigned long long n0 = ld_sc1(&A.normal[pixel].x), n1 = ld_sc1(&A.normal[pixel].z);
+                acc[0] = lo_f(i0);
+                acc[BLOCK] = hi_f(i0);
+                acc[2 * BLOCK] = lo_f(i1);
+                acc[3 * BLOCK] = hi_f(i1);
+                acc[4 * BLOCK] = lo_f(a0);
+                acc[5 * BLOCK] = hi_f(a0);
+                acc[6 * BLOCK] = lo_f(a1);
+                acc[7 * BLOCK] = lo_f(n0);
+                acc[8 * BLOCK] = hi_f(n0);
+                acc[9 * BLOCK] = lo_f(n1);
+                acc_i[10 * BLOCK] = 0;
+                acc_i[11 * BLOCK] = c == 0 ? s_begin : cb_lds[c - 1];
+            }
+        }
+        // ---- every lane starting a sample (a new pixel, or the next sample of its pixel): the
+        // camera ray (trace_sample's prologue) and its query's first pops, where many lanes share them
+        next_sample = false;
+        if (start) {
+            const int sample = acc_i[11 * BLOCK];
+            if (!ft_none(F)) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+            start_path<F>(P, pixel % P.width, pixel / P.width, pixel, sample, st);
+            query_start<WIDE>(S, T, st.o, st.d, -1, stack);
+            if (!WC) lds_count(1, true);
+#if JT_ITEM_FIRST_POP
+#pragma unroll
+            for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
+                if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+#endif
+        }
+        if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(start));
+        if (__builtin_amdgcn_ballot_w64(item != ITEM_NONE) == 0) break;  // drained, and every lane is done
+        if (__builtin_amdgcn_ballot_w64(item != ITEM_NONE && !(item & ITEM_BLOCKED)) == 0) {
+            // every pixel held waits for its previous chunk (never expected: units are handed out
+            // chunk-major). Bounded: past the bound the wave flags the launch (counters[7], the
+            // host then fails it with JT_ERR_DEVICE) and starts the pixels rather than hang.
+            // (No `continue` here: a second back-edge of the loop made the register allocator
+            // spill 44-68 VGPRs of path state; with no lane active the phases below are no-ops.)
+            if (++spins == (1 << 22) && lane == 0) atomicAdd(A.counters + 7, 1ull);
+            __builtin_amdgcn_s_sleep(8);
+        }
+        // ---- traversal phase (as trace_body)
+        constexpr bool LSTEP = light_steps(SAMPLER, F);
+        for (;;) {
+            const bool wantp = T.nprim > 0;
+            const bool wantn = wants_node<WIDE>(T);
+            const bool waiting = query_done<WIDE>(T);
+            const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
+            const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
+            int nw = lane_count(__builtin_amdgcn_ballot_w64(waiting));
+            const int nb = np + nn;
+            if (LSTEP && !S.light_inline) {
+                const bool wantl = waiting && st.phase == PH_LIGHT;
+                const int nl = lane_count(__builtin_amdgcn_ballot_w64(wantl));
+                if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
+                    bool c_lq = false, c_ray = false;
+                    if (wantl) {
+                        if (light_hit<F>(S, P, st, query_hit(T))) {
+                            st.phase = PH_FINISH;
+                        } else if (st.phase == PH_LIGHT) {
+                            if (WC) c_lq = true;
+                            else lds_count(2, true);
+                            query_start<WIDE>(S, T, st.o, st.d, S.lights[st.li].instance, stack);
+                        } else {
+                            if (WC) c_ray = true;
+                            else lds_count(1, true);
+                            query_start<WIDE>(S, T, st.o, st.d, -1, stack);
+                        }
+                    }
+                    if (WC) {
+                        w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
+                        w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
+                    }
+                    continue;
+                }
+                nw -= nl;
+            }
+            if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
+            if (JT_RAY_FROM_PATH && !(F & FT_XFORM)) {
+                T.lo = st.o;
+                T.ld = st.d;
+            }
+            if (np * JT_VOTE_P >= nn * JT_VOTE_N) {
+                if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+            } else {
+                constexpr int NREP = ft_none(F) ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
+#pragma unroll
+                for (int k = 0; k < NREP; k++)
+                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+            }
+        }
+        // ---- shading phase: every waiting lane consumes its hit and issues its next query
+        bool c_path = false, c_lq = false, c_ray = false, c_done = false;
+        unsigned n_inl = 0;
+        if (query_done<WIDE>(T)) {
+            bool alive = true;
+            constexpr bool LINL = (F & (FT_LINL | FT_NOIL)) != 0;
+            const bool light = SAMPLER == 1 && !LINL && st.phase == PH_LIGHT;
+            bool done;
+            if (LSTEP && st.phase == PH_FINISH) done = true;
+            else if (light) done = light_hit<F>(S, P, st, query_hit(T));
+            else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
+            else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
+            if (SAMPLER == 1 && !done && st.phase == PH_LIGHT && chains_inline(F, S)) {
+                unsigned nlq = 0;
+                done = light_chain<WIDE, RING, OVF, COUNT, NCACHE, F>(S, P, st, T, stack, pixel, cnt, [&] {
+                    if (WC) nlq++;
+                    else lds_count(2, true);
+                });
+                if (WC) n_inl += nlq;
+            }
+            if (done) {
+                // trace_sample epilogue (src/trace.jl:625-648)
+                if (WC) c_path = true;
+                else lds_count(0, true);
+                v3 radiance = st.radiance<F>();
+                if (!all_finite(radiance)) radiance = V3(0, 0, 0);
+                const float mr = max3(radiance);
+                if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
+                const float w = aov.w<F>();
+                const float omw = 1 - w;
+                const bool hit = st.flag(F_HIT);
+                const bool env = !hit && !P.envhidden && S.nenvs != 0;
+                const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
+                if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
+                acc[0] = acc[0] * omw + target.x * w;
+                acc[BLOCK] = acc[BLOCK] * omw + target.y * w;
+                acc[2 * BLOCK] = acc[2 * BLOCK] * omw + target.z * w;
+                acc[3 * BLOCK] = acc[3 * BLOCK] * omw + target.w * w;
+                if (hit || env) acc_i[10 * BLOCK] += 1;
+                const int sample = acc_i[11 * BLOCK] + 1;
+                if (sample >= cb_lds[item_chunk(item)]) {
+                    // the pixel's chunk is complete: write-through its running means, hits at the memory side
+                    alive = false;
+                    T.sp = -1;
+                    st_sc1(&A.image[pixel].x, pack2(acc[0], acc[BLOCK]));
+                    st_sc1(&A.image[pixel].z, pack2(acc[2 * BLOCK], acc[3 * BLOCK]));
+                    st_sc1(&A.albedo[pixel].x, pack2(acc[4 * BLOCK], acc[5 * BLOCK]));
+                    st_sc1(&A.albedo[pixel].z, pack2(acc[6 * BLOCK], 0.0f));
+                    st_sc1(&A.normal[pixel].x, pack2(acc[7 * BLOCK], acc[8 * BLOCK]));
+                    st_sc1(&A.normal[pixel].z, pack2(acc[9 * BLOCK], 0.0f));
+                    if (acc_i[10 * BLOCK]) atomicAdd(reinterpret_cast<unsigned long long*>(A.hits + pixel),
+                                                     (unsigned long long)acc_i[10 * BLOCK]);
+                    c_done = true;
+                } else {
+                    acc_i[11 * BLOCK] = sample;  // started at the top of the next iteration
+                    alive = false;
+                    T.sp = -1;
+                    next_sample = true;
+                }
+            }
+            if (alive) {
+                if (SAMPLER == 1 && !LINL && st.phase == PH_LIGHT) {
+                    if (WC) c_lq = true;
+                    else lds_count(2, true);
+                    query_start<WIDE>(S, T, st.o, st.d, S.lights[st.li].instance, stack);
+                } else {
+                    if (WC) c_ray = true;
+                    else lds_count(1, true);
+                    query_start<WIDE>(S, T, st.o, st.d, -1, stack);
+                }
+#pragma unroll
+                for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
+                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+            }
+        }
+        if (WC) {
+            w_paths += lane_count(__builtin_amdgcn_ballot_w64(c_path));
+            w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
+            w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
+            if (SAMPLER == 1 && chains_inline(F, S)) w_lq += __builtin_amdgcn_readfirstlane(wave_sum(n_inl));
+        }
+        // publish the completed chunks: the wave's write-through stores drained, then each
+        // completing lane's done word (chunks accumulated of its pixel in this launch)
+        if (__builtin_amdgcn_ballot_w64(c_done)) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c_done) {
+                __hip_atomic_store(A.tile_done + (item & ITEM_SLOT_MASK), item_chunk(item) + 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                item = ITEM_NONE;
+            }
+        }
+    }
+    const unsigned wv[3] = {w_paths, w_rays, w_lq};
+    unsigned v[7] = {0u, 0u, 0u, cnt.nodes, cnt.instances, cnt.prims, COUNT ? cnt.shades : 0u};
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        unsigned sum = k < 3 ? (WC ? wv[k] : wcnt[k]) : wave_sum(v[k]);
+        if (lane == 0 && sum) atomicAdd(&A.counters[k], (unsigned long long)sum);
+    }
+}
+
 // Occupancy request (waves per SIMD); JT_WAVES=0 leaves it to the compiler. The LDS-mode
 // FT_NONE kernel (cornellbox: 96 VGPRs, LDS for 5 workgroups per CU with the stack sized to the
 // scene) asks for JT_WAVES_NONE: measured +4 % over 4 waves with its wait_lanes of 56.
@@ -1772,7 +2097,10 @@ __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob)
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool WIDE>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     __shared__ int lds_stack[RING * BLOCK];
-    trace_body<SAMPLER, RING, OVF, COUNT, F, true, WIDE>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
+    if constexpr (JT_LANE_ITEMS && !JT_STAMPS)
+        trace_body_items<SAMPLER, RING, OVF, COUNT, F, true, WIDE>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
+    else
+        trace_body<SAMPLER, RING, OVF, COUNT, F, true, WIDE>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
 }
 
 // LDS mode (small scenes): the workgroup stages the scene blob into LDS once; every node,
@@ -1786,7 +2114,10 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(D
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
     const DScene L = blob_scene(S, blob);
-    trace_body<SAMPLER, RING, OVF, COUNT, F, false, WIDE>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+    if constexpr (JT_LANE_ITEMS && !JT_STAMPS)
+        trace_body_items<SAMPLER, RING, OVF, COUNT, F, false, WIDE>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+    else
+        trace_body<SAMPLER, RING, OVF, COUNT, F, false, WIDE>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of

@@ -351,6 +351,10 @@ int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_wo
     return rec[0];
 }
 
+// the launch schedule: a unit counter per XCD band, then a done word per pixel slot (tile * 64 + l:
+// chunks accumulated in this launch; the tile-unit body uses one word per tile, the first tiles)
+size_t sched_bytes(int tiles) { return ((size_t)tiles * 64 + NBANDS * BAND_STRIDE) * 4; }
+
 int check_tree(const jt_bvh_tree& t, int nprims_expected, const char* what) {
     if (t.nprimitives != nprims_expected) return jt::fail(JT_ERR_INVALID, std::string(what) + ": primitive count mismatch");
     for (int k = 0; k < t.nnodes; k++) {
@@ -1024,9 +1028,10 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     P.seed = params->seed;
     P.tile_stride = 1;  // every tile (jt_create_multi may split by tiles)
     P.tile_offset = 0;
-    // option test_tiles "stride,offset" (tests only): trace only tiles offset, offset + stride,
-    // ... — one device's share of a tile-split multi-device context, reproducible on one GPU
-    if (const char* ts = opt("test_tiles")) {
+    // option tile_share "stride,offset": trace only tiles offset, offset + stride, ... — one
+    // process's share of a render split by tiles over one process per GPU (bench.py), or one
+    // device's share of jt_create_multi's tile split reproduced on one GPU (tests)
+    if (const char* ts = opt("tile_share")) {
         int k = 0, o = 0;
         if (std::sscanf(ts, "%d,%d", &k, &o) == 2 && k >= 1 && o >= 0 && o < k) {
             P.tile_stride = k;
@@ -1071,10 +1076,12 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     c->allocations.push_back(hits);
     if ((e = hipMalloc(&cnt, 32 * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc counters"));
     c->allocations.push_back(cnt);
-    // persistent scheduling: unit counter + per-tile chunk counters (zeroed before each launch)
+    // persistent scheduling: unit counters + per-pixel chunk counters (zeroed before each launch)
     c->tiles = ((W + 7) / 8) * ((H + 7) / 8);
+    if (c->tiles >= (1 << 20))  // the per-lane work items address a pixel as tile * 64 + l in 26 bits
+        return bail(jt::fail(JT_ERR_UNSUPPORTED, "image above 2^20 8x8 tiles (67 Mpixels)"));
     void* sched = nullptr;
-    if ((e = hipMalloc(&sched, (size_t)(c->tiles + NBANDS * BAND_STRIDE) * 4)) != hipSuccess)
+    if ((e = hipMalloc(&sched, sched_bytes(c->tiles))) != hipSuccess)
         return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc schedule"));
     c->allocations.push_back(sched);
     int cus = 0;
@@ -1125,7 +1132,7 @@ int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lig
         if (m != opts.end() && m->second == "tiles") c->tile_split = true;
         if (m != opts.end() && m->second == "samples") c->tile_split = false;
     }
-    // every sub-context traces every tile under the sample split (a test_tiles option never
+    // every sub-context traces every tile under the sample split (a tile_share option never
     // leaves tiles out of the reduced image), its interleaved share under the tile split
     for (int d = 0; d < ndevices; d++) {
         c->sub[d]->P.tile_stride = c->tile_split ? ndevices : 1;
@@ -1221,6 +1228,8 @@ int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
     // (profiles/r02_chunk_tail.txt)
     const int cmin = c->chunk_min >= 0 ? c->chunk_min : (c->lds_scene_bytes > 0 && c->P.chunk >= 32 ? c->P.chunk / 2 : 0);
     c->P.nct = 0;
+    // at most JT_MAX_CHUNKS chunks per launch (the per-lane work items keep a pixel's chunk in 5 bits)
+    if ((nsamp + c->P.chunk - 1) / c->P.chunk > JT_MAX_CHUNKS) c->P.chunk = (nsamp + JT_MAX_CHUNKS - 1) / JT_MAX_CHUNKS;
     if (cmin > 0 && cmin < c->P.chunk) {
         int rem = s1 - s0, n = 0, at = 0;
         c->P.cbeg[0] = 0;
@@ -1234,7 +1243,7 @@ int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
         if (rem == 0) c->P.nct = n;
     }
     (void)hipSetDevice(c->device);
-    hipError_t e = hipMemsetAsync(c->A.work, 0, (size_t)(c->tiles + NBANDS * BAND_STRIDE) * 4, c->stream);
+    hipError_t e = hipMemsetAsync(c->A.work, 0, sched_bytes(c->tiles), c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
     // counter [7] counts this launch's tile-order wait timeouts only
     if ((e = hipMemsetAsync(c->A.counters + 7, 0, 8, c->stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");

@@ -22,6 +22,19 @@ def shard_range(total_samples: int, world: int, rank: int) -> tuple[int, int]:
     return rank * total_samples // world, (rank + 1) * total_samples // world
 
 
+def split_plan(world: int, rank: int, total_samples: int, tile_groups: int):
+    """Rank `rank`'s share of a render over `world` processes split into `tile_groups` interleaved
+    8x8-tile groups (a power of two dividing world; 1 = a pure sample split) times world /
+    tile_groups contiguous sample ranges: (tile_share option value or None, s0, s1). Every pixel is
+    covered by world / tile_groups ranks whose sample ranges partition [0, total_samples), so the
+    same sample-weighted reduce (reduce_running_means) combines any plan."""
+    if tile_groups < 1 or world % tile_groups:
+        raise ValueError(f"tile_groups {tile_groups} must divide world {world}")
+    g, k = rank % tile_groups, rank // tile_groups
+    s0, s1 = shard_range(total_samples, world // tile_groups, k)
+    return (f"{tile_groups},{g}" if tile_groups > 1 else None), s0, s1
+
+
 def reduce_running_means(tensor, n_local: int, n_total: int, dist, dst: int = 0):
     """Sum-reduce sample-weighted shard means onto `dst`; returns the combined mean on `dst`
     (the partial sum elsewhere). `tensor` is left untouched."""

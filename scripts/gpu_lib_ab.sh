@@ -10,7 +10,7 @@ args() {
     f2) echo "--scene assets/scenes/features2/features2.json --width 1920 --height 1080 --spp ${AB_F2_SPP:-64}" ;;
     b1) echo "--scene assets/scenes/bathroom1/bathroom1.json --width 1920 --height 1080 --spp ${AB_B1_SPP:-64}" ;;
     ec) echo "--scene assets/scenes/ecosys/ecosys.json --width 3840 --height 2160 --spp ${AB_EC_SPP:-8}" ;;
-    cb) echo "" ;;
+    cb) echo "--steps 10" ;;
   esac
 }
 for rep in 1 2; do

@@ -66,7 +66,7 @@ def test_run_time_options_are_explicit(abi, lib):
     assert lib.jt_set_option(b"no_such_option", b"1") == -1
     assert b"unknown option" in lib.jt_last_error()
     for name in ("env_alias", "features", "lds_scene", "lds_stack", "light_inline", "chunk", "chunk_min",
-                 "wait_lanes", "light_lanes", "multi_split", "test_tiles", "test_lds_ring"):
+                 "wait_lanes", "light_lanes", "multi_split", "tile_share", "test_lds_ring"):
         assert lib.jt_set_option(name.encode(), b"1") == 0
         assert lib.jt_set_option(name.encode(), None) == 0
     assert lib.jt_set_option(None, b"1") == -1

@@ -67,7 +67,7 @@ def test_multi_context_rejects_bad_device_lists(gpu, abi, lib, cornell_abi):
 @pytest.mark.parametrize("D", [2, 3, 8])
 def test_tile_split_shares_sum_to_the_single_device_image(gpu, abi, lib, cornell_abi, D, options):
     """The tile split of jt_create_multi at batch < devices, reproduced on one GPU: contexts
-    tracing every D-th 8x8 tile from offset d (option test_tiles, the per-device launch parameters the
+    tracing every D-th 8x8 tile from offset d (option tile_share, the per-device launch parameters the
     multi-device context sets) at the reference's default --batch 1 each cover disjoint pixels,
     every one of them traces work, and their plain sum is the single-device image bit for bit."""
     p = make_params(abi, resolution=72, samples=3, batch=1)
@@ -77,7 +77,7 @@ def test_tile_split_shares_sum_to_the_single_device_image(gpu, abi, lib, cornell
     hits = np.zeros_like(one[1][2])
     paths = 0
     for d in range(D):
-        options("test_tiles", f"{D},{d}")
+        options("tile_share", f"{D},{d}")
         part = _render(abi, lib, cornell_abi, p, 3)
         assert part[2]["paths"] > 0, d  # every device gets work at batch 1
         paths += part[2]["paths"]
