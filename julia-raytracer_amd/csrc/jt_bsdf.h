@@ -363,6 +363,44 @@ __device__ __forceinline__ float sample_bsdfcos_pdf(const MatPoint& m, v3 n, v3 
         default: return 0;
     }
 }
+// eval_bsdfcos and sample_bsdfcos_pdf of one (material, n, o, i), evaluated in ONE branch per
+// material type (material-keyed shading): the two reference functions run back to back
+// on every non-delta bounce (src/trace.jl:386-392); as two switches a wave executes each present
+// type's code region twice, once per switch; here once, and the compiler shares what the two compute
+// alike (dot products, Fresnel terms, the GGX distribution). The same float operations in the same
+// order per function, so results are unchanged.
+template <int F>
+__device__ __forceinline__ void eval_bsdfcos_pdf(const MatPoint& m, v3 n, v3 o, v3 i, v3& f, float& pdf) {
+    f = V3(0, 0, 0);
+    pdf = 0;
+    if (m.roughness == 0) return;
+    switch (m.type) {
+        case M_MATTE:
+            f = eval_matte(m.color, n, o, i);
+            pdf = sample_matte_pdf(n, o, i);
+            return;
+        case M_GLOSSY:
+            f = eval_glossy(m.color, m.ior, m.roughness, n, o, i);
+            pdf = sample_glossy_pdf(m.ior, m.roughness, n, o, i);
+            return;
+        case M_REFLECTIVE:
+            f = eval_reflective(m.color, m.roughness, n, o, i);
+            pdf = sample_reflective_pdf(m.roughness, n, o, i);
+            return;
+        case M_TRANSPARENT:
+            f = eval_transparent(m.color, m.ior, m.roughness, n, o, i);
+            pdf = sample_transparent_pdf(m.ior, m.roughness, n, o, i);
+            return;
+        case M_REFRACTIVE:
+        case M_SUBSURFACE:
+            if (F & FT_VOL) {
+                f = eval_refractive(m.ior, m.roughness, n, o, i);
+                pdf = sample_refractive_pdf(m.ior, m.roughness, n, o, i);
+            }
+            return;
+        default: return;
+    }
+}
 template <int F>
 __device__ __forceinline__ v3 eval_delta(const MatPoint& m, v3 n, v3 o, v3 i) {  // :757-778
     if (m.roughness != 0) return V3(0, 0, 0);

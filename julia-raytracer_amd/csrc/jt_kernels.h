@@ -57,6 +57,10 @@
 #ifndef JT_CHILD_PRETEST
 #define JT_CHILD_PRETEST 1
 #endif
+// eval_bsdfcos + sample_bsdfcos_pdf in one branch per material type (jt_bsdf.h eval_bsdfcos_pdf)
+#ifndef JT_FUSED_BSDF
+#define JT_FUSED_BSDF 1
+#endif
 #ifndef JT_RAY_FROM_PATH
 #define JT_RAY_FROM_PATH 1
 #endif
@@ -1146,8 +1150,16 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
                 incoming = sample_lights<F>(S, sh.position, rl, rel, ruv);
             }
             if (is_zero(incoming)) return true;
+#if JT_FUSED_BSDF
+            v3 fb;
+            float pbv;
+            eval_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming, fb, pbv);
+            st.weight = st.weight * fb;
+            st.set_pb<F>(pbv);
+#else
             st.weight = st.weight * eval_bsdfcos<F>(sh.mat, sh.normal, outgoing, incoming);
             st.set_pb<F>(sample_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming));
+#endif
         } else {
             float rnl = rand1f(st.rng);
             incoming = sample_delta<F>(sh.mat, sh.normal, outgoing, rnl);
@@ -1224,8 +1236,12 @@ __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Pat
         v2 rn = rand2f(st.rng);
         incoming = sample_bsdfcos<F>(sh.mat, sh.normal, outgoing, rnl, rn);
         if (is_zero(incoming)) return true;
+#if JT_FUSED_BSDF
+        eval_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming, f, p);
+#else
         f = eval_bsdfcos<F>(sh.mat, sh.normal, outgoing, incoming);
         p = sample_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
+#endif
     } else {
         float rnl = rand1f(st.rng);
         incoming = sample_delta<F>(sh.mat, sh.normal, outgoing, rnl);
