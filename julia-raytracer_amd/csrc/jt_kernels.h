@@ -680,13 +680,14 @@ __device__ __forceinline__ void wide_box(const float4& r0, const uint4& r1, cons
 // of children whose boxes passed, 0-23 the record) — or an instance range (bit 31 set; bits 24-25
 // count - 1, 0-23 the first instance) of a TLAS leaf whose first instance is being visited.
 // A child whose box passed is visited even if tmax has shrunk since (no re-test at pop).
+// (Every field is written on both paths: as two branches storing to different fields, the
+// compiler merged the stores into one through a selected address, and the Trav fields it addressed
+// no longer fit in registers — they lived in scratch, stored per node step.)
 __device__ __forceinline__ void wide_take(Trav& T, unsigned w) {
-    if ((w & (W_LEAF | W_INST)) == W_LEAF) {  // a BLAS leaf: its primitives are tested next, in order
-        T.prim = (int)(w & W_START);
-        T.nprim = (int)((w >> 28) & 3u) + 1;
-    } else {
-        T.nxt = w;  // a record, or a TLAS leaf (its first instance is visited by the next step)
-    }
+    const bool leaf = (w & (W_LEAF | W_INST)) == W_LEAF;  // a BLAS leaf: its primitives are tested next
+    T.prim = leaf ? (int)(w & W_START) : T.prim;
+    T.nprim = leaf ? (int)((w >> 28) & 3u) + 1 : T.nprim;
+    T.nxt = leaf ? T.nxt : w;  // a record, or a TLAS leaf (its first instance is visited by the next step)
 }
 // one record visit: the up-to-four child boxes against the current ray and tmax; the first passing
 // child (visit order) is taken at once, the others are pushed as one group entry

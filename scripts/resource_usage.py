@@ -15,6 +15,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=o
          "-DJT_EXACT_MATH=1", "-fno-slp-vectorize", "-mllvm", "-sink-insts-to-avoid-spills=1", "-DJT_WAVES=4"]
 NAMES = ["FT_NONE+LINL", "FT_ALL", "FT_MESH+LINL", "FT_MESH_ENV+NOIL", "FT_MESH_ENV_QUAD+LINL", "FT_ALL ovf", "FT_ALL ring32",
          "FT_NONE lsteps"]
+NAMES += [n + " wide" for n in NAMES]  # configurations 8-15: the wide traversal
 
 
 def usage(v, extra):
@@ -59,11 +60,11 @@ def loop_scratch_stores(asm, name):
 def main():
     extra = sys.argv[1:]
     with ThreadPoolExecutor(7) as ex:
-        res = list(ex.map(lambda v: usage(v, extra), range(8)))
+        res = list(ex.map(lambda v: usage(v, extra), range(len(NAMES))))
     print(f"{'config':22} {'kernel':16} {'sampler':7} {'VGPRs':>5} {'spill':>5} {'scratch':>7} {'occ':>3} {'loop stores':>11}")
     for v, rows in res:
         for r in rows:
-            m = re.search(r"(trace_kernel\w*)ILi(\d)ELi(\d+)ELb(\d)ELi(\d)ELi(\d+)E", r["name"])
+            m = re.search(r"(trace_kernel\w*)ILi(\d)ELi(\d+)ELb(\d)ELi(\d)ELi(\d+)ELb(\d)E", r["name"])
             if not m or m.group(5) != "0":
                 continue
             print(f"{NAMES[v]:22} {m.group(1):16} {m.group(2):7} {r.get('VGPRs', 0):5} {r.get('VGPRs Spill', 0):5} "

@@ -161,7 +161,7 @@ def test_feature_specialisation_bitwise_equal(gpu, abi, lib, cornell_abi, sample
         st.trace_range(0, 4)
         outs.append((st.get_image(), st.get_aovs(), st.counters(), st.describe()))
         st.close()
-    assert ",8192> " in outs[0][3] and ",255> " in outs[1][3], (outs[0][3], outs[1][3])  # FT_NONE | FT_LINL
+    assert ",8192," in outs[0][3] and ",255," in outs[1][3], (outs[0][3], outs[1][3])  # FT_NONE | FT_LINL
     assert np.array_equal(outs[0][0], outs[1][0])
     for a, b in zip(outs[0][1], outs[1][1]):
         assert np.array_equal(a, b)

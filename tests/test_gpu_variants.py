@@ -77,4 +77,4 @@ def test_vertex_colors_parity(gpu, abi, lib, oracle, cornell, sampler):
         col[:, 3] = 1.0 if k % 2 else rng.uniform(0.6, 1.0, size=n).astype(np.float32)
         s.colors = col
     g, o = _parity(abi, lib, oracle, sc, f"vcolor/{sampler}", sampler=sampler)
-    assert ",255> " in g[5]  # FT_ATTR | FT_OPAC: the general kernel
+    assert ",255," in g[5]  # FT_ATTR | FT_OPAC: the general kernel
