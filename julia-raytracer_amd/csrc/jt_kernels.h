@@ -334,7 +334,8 @@ __device__ __forceinline__ v3 eval_environment(const DScene& S, v3 direction) {
 // pushed (SNAP_NONE: not pre-tested). Layout stack[k * BLOCK + lane]:
 // every lane owns one bank (conflict-free ds_read/write_b32 whatever the per-lane depth).
 // The LDS part is a ring of RING entries; when a scene's bound exceeds it (OVF), the oldest
-// entries spill to a per-pixel HBM area and come back one at a time when popped.
+// entries spill to a per-lane HBM area (slot blockIdx.x * BLOCK + threadIdx.x of the persistent
+// grid: a query never outlives its lane) and come back one at a time when popped.
 constexpr int BLOCK = 256;
 constexpr unsigned T_TLAS = 0u, T_INST = 1u, T_BLAS = 2u;
 constexpr unsigned IDX_MASK = (1u << 24) - 1;
@@ -1384,6 +1385,7 @@ template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, bool W
 __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
                                            int* stack) {
     const int lane = threadIdx.x & 63;
+    const int oslot = (int)blockIdx.x * BLOCK + (int)threadIdx.x;  // the lane's HBM stack-overflow area
     if constexpr ((F & (FT_TEX | FT_ENV)) != 0) {  // the texel-decode LUTs into LDS (tex_lut)
         for (int k = threadIdx.x; k < 512; k += BLOCK) tex_lut[k] = k < 256 ? S.srgb_lut[k] : S.byte_lut[k - 256];
         __syncthreads();
@@ -1547,7 +1549,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 constexpr int NREP = ft_none(F) ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
 #pragma unroll
                 for (int k = 0; k < NREP; k++)
-                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
             }
         }
 #if JT_STAMPS
@@ -1606,7 +1608,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #endif
             if (SAMPLER == 1 && !done && st.phase == PH_LIGHT && chains_inline(F, S)) {
                 unsigned nlq = 0;
-                done = light_chain<WIDE, RING, OVF, COUNT, NCACHE, F>(S, P, st, T, stack, pixel, cnt, [&] {
+                done = light_chain<WIDE, RING, OVF, COUNT, NCACHE, F>(S, P, st, T, stack, oslot, cnt, [&] {
                     if (WC) nlq++;
                     else lds_count(2, true);
                 });
@@ -1674,7 +1676,7 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
                 // where most of the wave's lanes take part, rather than in a sparser traversal step
 #pragma unroll
                 for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
-                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
             }
 #if JT_STAMPS
             t_qb += __builtin_amdgcn_s_memtime() - s3;
@@ -1781,11 +1783,17 @@ __device__ __forceinline__ unsigned long long pack2(float a, float b) {
 __device__ __forceinline__ float lo_f(unsigned long long v) { return __uint_as_float((unsigned)v); }
 __device__ __forceinline__ float hi_f(unsigned long long v) { return __uint_as_float((unsigned)(v >> 32)); }
 
+// the image index of an item's pixel (its slot holds the global tile and the pixel of the tile)
+__device__ __forceinline__ int item_pixel(unsigned item, const DParams& P, int tiles_x) {
+    const int slot = (int)(item & ITEM_SLOT_MASK), t = slot >> 6, l = slot & 63;
+    return ((t / tiles_x) * 8 + (l >> 3)) * P.width + (t % tiles_x) * 8 + (l & 7);
+}
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, bool WIDE>
 __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams& P, int s_begin, int s_end,
                                                  const DAccum& A, int* stack) {
     static_assert(lane_lds(F), "the per-lane item body keeps the lane's sample index in LDS");
     const int lane = threadIdx.x & 63;
+    const int oslot = (int)blockIdx.x * BLOCK + (int)threadIdx.x;  // the lane's HBM stack-overflow area
     if constexpr ((F & (FT_TEX | FT_ENV)) != 0) {  // the texel-decode LUTs into LDS (tex_lut)
         for (int k = threadIdx.x; k < 512; k += BLOCK) tex_lut[k] = k < 256 ? S.srgb_lut[k] : S.byte_lut[k - 256];
     }
@@ -1820,7 +1828,6 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
     unsigned item = ITEM_NONE;       // the lane's pixel (ITEM_* above)
     int spins = 0;                   // iterations in which every held pixel waited (bounded)
     bool next_sample = false;        // the lane's next sample starts at the top of the iteration
-    int pixel = 0;                   // its image index (RNG key, HBM stack overflow area)
     Aov aov{acc, 0.0f, P.first};
     Path st;
     st.pk = acc + acc_base_slots(F) * BLOCK;
@@ -1853,10 +1860,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 const int l = bnext + rank;
                 const int i = (ut % tiles_x) * 8 + (l & 7), j = (ut / tiles_x) * 8 + (l >> 3);
                 // a pixel outside the image (edge tiles) is skipped: the lane takes another
-                if (i < P.width && j < P.height) {
-                    item = (unsigned)(ut * 64 + l) | (unsigned)uc << ITEM_CHUNK_SHIFT | ITEM_BLOCKED;
-                    pixel = j * P.width + i;
-                }
+                if (i < P.width && j < P.height) item = (unsigned)(ut * 64 + l) | (unsigned)uc << ITEM_CHUNK_SHIFT | ITEM_BLOCKED;
             }
             bnext += take;
         }
@@ -1869,6 +1873,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 __hip_atomic_load(A.tile_done + (item & ITEM_SLOT_MASK), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c) {
                 start = true;
                 item &= ~ITEM_BLOCKED;
+                const int pixel = item_pixel(item, P, tiles_x);
                 const unsigned long long i0 = ld_sc1(&A.image[pixel].x), i1 = ld_sc1(&A.image[pixel].z);
                 const unsigned long long a0 = ld_sc1(&A.albedo[pixel].x), a1 = ld_sc1(&A.albedo[pixel].z);
                 const unsigned long long n0 = ld_sc1(&A.normal[pixel].x), n1 = ld_sc1(&A.normal[pixel].z);
@@ -1891,6 +1896,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
         next_sample = false;
         if (start) {
             const int sample = acc_i[11 * BLOCK];
+            const int pixel = item_pixel(item, P, tiles_x);
             if (!ft_none(F)) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
             start_path<F>(P, pixel % P.width, pixel / P.width, pixel, sample, st);
             query_start<WIDE>(S, T, st.o, st.d, -1, stack);
@@ -1898,7 +1904,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
 #if JT_ITEM_FIRST_POP
 #pragma unroll
             for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
-                if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+                if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
 #endif
         }
         if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(start));
@@ -1959,7 +1965,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 constexpr int NREP = ft_none(F) ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
 #pragma unroll
                 for (int k = 0; k < NREP; k++)
-                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
             }
         }
         // ---- shading phase: every waiting lane consumes its hit and issues its next query
@@ -1976,7 +1982,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
             else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
             if (SAMPLER == 1 && !done && st.phase == PH_LIGHT && chains_inline(F, S)) {
                 unsigned nlq = 0;
-                done = light_chain<WIDE, RING, OVF, COUNT, NCACHE, F>(S, P, st, T, stack, pixel, cnt, [&] {
+                done = light_chain<WIDE, RING, OVF, COUNT, NCACHE, F>(S, P, st, T, stack, oslot, cnt, [&] {
                     if (WC) nlq++;
                     else lds_count(2, true);
                 });
@@ -2006,6 +2012,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                     // the pixel's chunk is complete: write-through its running means, hits at the memory side
                     alive = false;
                     T.sp = -1;
+                    const int pixel = item_pixel(item, P, tiles_x);
                     st_sc1(&A.image[pixel].x, pack2(acc[0], acc[BLOCK]));
                     st_sc1(&A.image[pixel].z, pack2(acc[2 * BLOCK], acc[3 * BLOCK]));
                     st_sc1(&A.albedo[pixel].x, pack2(acc[4 * BLOCK], acc[5 * BLOCK]));
@@ -2034,7 +2041,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 }
 #pragma unroll
                 for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
-                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
             }
         }
         if (WC) {
@@ -2153,14 +2160,14 @@ hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAc
         const void* k = (const void*)trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F, WIDE>;
         if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-        const int nwg = std::min(want, per_cu * cus);
+        const int nwg = std::min(want, std::min(per_cu, 8) * cus);  // <= 8 per CU: the overflow area's bound
         hipLaunchKernelGGL((trace_kernel_lds<SAMPLER, RING, OVF, COUNT, F, WIDE>), dim3(nwg), dim3(BLOCK), lds, st, S, P, s0, s1, A);
         return hipGetLastError();
         }
     }
     const void* k = (const void*)trace_kernel<SAMPLER, RING, OVF, COUNT, F, WIDE>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BLOCK, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    const int nwg = std::min(want, per_cu * cus);
+    const int nwg = std::min(want, std::min(per_cu, 8) * cus);
     hipLaunchKernelGGL((trace_kernel<SAMPLER, RING, OVF, COUNT, F, WIDE>), dim3(nwg), dim3(BLOCK), 0, st, S, P, s0, s1, A);
     return hipGetLastError();
 }

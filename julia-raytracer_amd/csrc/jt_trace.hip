@@ -994,9 +994,14 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             c->ring = 16;
         }
     }
-    if (c->stack > 16) {  // HBM overflow of the LDS stack ring: `need` entries per pixel
+    if (c->stack > 16) {  // HBM overflow of the LDS stack ring: `need` entries per lane of the
+        // persistent grid (at most 8 workgroups of BLOCK lanes per CU resident; kernel slot
+        // blockIdx.x * BLOCK + threadIdx.x: a query never outlives its lane)
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, params->device) != hipSuccess || ncu < 1)
+            ncu = 256;
         void* p = nullptr;
-        const size_t bytes = (size_t)W * (size_t)H * (size_t)need * 4;
+        const size_t bytes = (size_t)ncu * 8 * BLOCK * (size_t)need * 4;
         if ((e = hipMalloc(&p, bytes)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc stack overflow"));
         c->allocations.push_back(p);
         S.ovf = (int*)p;
