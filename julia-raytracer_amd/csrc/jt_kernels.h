@@ -668,13 +668,17 @@ __device__ __forceinline__ unsigned wide_word(const uint4& r3, int slot) {
     return slot == 0 ? r3.x : slot == 1 ? r3.y : slot == 2 ? r3.z : r3.w;
 }
 // dequantised box of slot c (the record's origin + byte * scale, in float) as intersect_bbox's
-// (bmin.x, bmax.x, bmin.y, bmax.y), (bmin.z, bmax.z)
+// (bmin.x, bmax.x, bmin.y, bmax.y), (bmin.z, bmax.z). byte * scale is exact (a byte times a
+// normal power of two), so the fused multiply-add rounds once exactly as origin + byte * scale
+// does: one v_fma_f32 per plane, the same bits as the host's quantisation check.
+__device__ __forceinline__ float deq(float o, unsigned w, int sh, float s) {
+    return __builtin_fmaf((float)((w >> sh) & 255u), s, o);
+}
 __device__ __forceinline__ void wide_box(const float4& r0, const uint4& r1, const uint4& r2, float sx, float sy,
                                          float sz, int c, float4& a, float4& b) {
     const int sh = 8 * c;
-    a = make_float4(r0.x + (float)((r1.x >> sh) & 255u) * sx, r0.x + (float)((r1.y >> sh) & 255u) * sx,
-                    r0.y + (float)((r1.z >> sh) & 255u) * sy, r0.y + (float)((r1.w >> sh) & 255u) * sy);
-    b = make_float4(r0.z + (float)((r2.x >> sh) & 255u) * sz, r0.z + (float)((r2.y >> sh) & 255u) * sz, 0.0f, 0.0f);
+    a = make_float4(deq(r0.x, r1.x, sh, sx), deq(r0.x, r1.y, sh, sx), deq(r0.y, r1.z, sh, sy), deq(r0.y, r1.w, sh, sy));
+    b = make_float4(deq(r0.z, r2.x, sh, sz), deq(r0.z, r2.y, sh, sz), 0.0f, 0.0f);
 }
 // Stack entries of the wide traversal (32 bits): a group — the children of record `index` still
 // to visit (bit 31 clear; bits 28-30 the record's flips for this ray, 24-27 the visit-order mask

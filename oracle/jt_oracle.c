@@ -601,7 +601,7 @@ static void w_test(const wrec_t* w, const ray3* ray, v3 dinv, int* hit) {
         hit[k] = 0;
         if (w->child[k] < 0) continue;
         float bmin[3], bmax[3];
-        for (int ax = 0; ax < 3; ax++) {
+        for (int ax = 0; ax < 3; ax++) {  /* byte * scale is exact: one rounding, as the kernel's fma */
             bmin[ax] = w->o[ax] + (float)w->lo[ax][k] * w->s[ax];
             bmax[ax] = w->o[ax] + (float)w->hi[ax][k] * w->s[ax];
         }
