@@ -65,3 +65,23 @@ def test_shard_ranges_cover_all_samples():
         for N in (1, 2, 3, 8):
             r = [shard_range(S, N, k) for k in range(N)]
             assert r[0][0] == 0 and r[-1][1] == S and all(r[k][1] == r[k + 1][0] for k in range(N - 1))
+
+
+def test_split_plans_partition_every_pixel_sample():
+    """bench.py's hybrid split (jtrace.parallel.split_plan): G interleaved tile groups x N/G
+    contiguous sample ranges. Every (tile, sample) is traced by exactly one rank, and the ranks
+    covering a tile partition [0, S), so one sample-weighted reduce combines any plan."""
+    from jtrace.parallel import split_plan
+    tiles, S = 37, 256
+    for N in (1, 2, 4, 8):
+        G = 1
+        while G <= N:
+            cover = np.zeros((tiles, S), int)
+            for r in range(N):
+                share, s0, s1 = split_plan(N, r, S, G)
+                k, o = (1, 0) if share is None else map(int, share.split(","))
+                cover[o::k, s0:s1] += 1
+            assert (cover == 1).all(), (N, G)
+            G *= 2
+    with pytest.raises(ValueError):
+        split_plan(8, 0, S, 3)
