@@ -105,7 +105,7 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--sampler", default="path")
     ap.add_argument("--scene", default=str(ROOT / "assets" / "scenes" / "cornellbox" / "cornellbox.json"))
-    ap.add_argument("--traversal", choices=["reference", "near", "wide"], default=DEFAULT_TRAVERSAL,
+    ap.add_argument("--traversal", choices=["reference", "near", "wide", "auto"], default=DEFAULT_TRAVERSAL,
                     help="BVH child order (include/jtrace.h jt_traversal): near child first (the default, the "
                          "product's order) or the reference's far-first order (src/bvh.jl:331-341)")
     ap.add_argument("--no-reference-order", action="store_true",

@@ -87,7 +87,9 @@ typedef enum jt_sampler { JT_SAMPLER_PATH = 1, JT_SAMPLER_NAIVE = 2 } jt_sampler
 typedef enum jt_traversal {
     JT_TRAVERSAL_REFERENCE = 0,
     JT_TRAVERSAL_NEAR = 1,
-    JT_TRAVERSAL_WIDE = 2
+    JT_TRAVERSAL_WIDE = 2,
+    JT_TRAVERSAL_AUTO = 3  /* near for a scene small enough to run from LDS, wide otherwise;
+                              jt_describe reports the order taken ("traversal=near|wide") */
 } jt_traversal;
 
 /* CameraData (src/scene.jl:48-86), after the lookat conversion done by the loader. */

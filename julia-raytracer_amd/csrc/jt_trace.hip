@@ -87,6 +87,7 @@ struct jt_ctx {
     int feat = FT_ALL;   // scene feature bits (jt_device.h)
     int kmask = FT_ALL;  // feature mask of the kernel specialisation the scene runs
     bool wide = false;   // JT_TRAVERSAL_WIDE: the wide-record kernels (configurations 8-15)
+    int traversal = 0;   // jt_params.traversal as resolved (JT_TRAVERSAL_AUTO: near or wide)
     int first = -1, next = 0;  // running-mean origin and next expected sample
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     bool failed = false;       // a launch's tile-order wait timed out: the running means are unusable
@@ -706,21 +707,21 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         }
     }
     // wide records (JT_TRAVERSAL_WIDE): the TLAS's, then every BLAS's; the binary node array is
-    // then not uploaded
-    if (params->traversal != JT_TRAVERSAL_REFERENCE && params->traversal != JT_TRAVERSAL_NEAR &&
-        params->traversal != JT_TRAVERSAL_WIDE)
-        return bail(jt::fail(JT_ERR_INVALID, "traversal must be 0 (reference), 1 (near) or 2 (wide)"));
+    // then not uploaded. JT_TRAVERSAL_AUTO resolves to near for a small scene that runs from LDS
+    // and to wide otherwise (decided with the LDS blob below; the records are built then).
+    if (params->traversal < JT_TRAVERSAL_REFERENCE || params->traversal > JT_TRAVERSAL_AUTO)
+        return bail(jt::fail(JT_ERR_INVALID, "traversal must be 0 (reference), 1 (near), 2 (wide) or 3 (auto)"));
     c->wide = params->traversal == JT_TRAVERSAL_WIDE;
     std::vector<DWide> wnodes;
     std::vector<int> wroot(scene->nshapes, 0);
     int tlas_wnodes = 0;
-    if (c->wide) {
+    auto build_all_wide = [&]() -> int {
         const int r = build_wide(bvh->tlas, [&](int k) -> unsigned {
             const jt_bvh_node& n = bvh->tlas.nodes[k];
             if (n.start < 0 || n.start > (int)W_START - 1) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: instance id too large"), (unsigned)W_EMPTY;
             return W_LEAF | W_INST | (unsigned)(n.num - 1) << 28 | (unsigned)n.start;
         }, wnodes);
-        if (r < 0) return bail(JT_ERR_UNSUPPORTED);
+        if (r < 0) return JT_ERR_UNSUPPORTED;
         tlas_wnodes = (int)wnodes.size();
         for (int s = 0; s < scene->nshapes; s++) {
             const jt_bvh_tree& t = bvh->blas[s];
@@ -729,9 +730,11 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                 if (st0 < 0 || st0 > (int)W_START - 1) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: too many primitive records"), (unsigned)W_EMPTY;
                 return W_LEAF | (unsigned)(t.nodes[k].num - 1) << 28 | (unsigned)st0;
             }, wnodes);
-            if (wroot[s] < 0) return bail(JT_ERR_UNSUPPORTED);
+            if (wroot[s] < 0) return JT_ERR_UNSUPPORTED;
         }
-    }
+        return JT_OK;
+    };
+    if (c->wide && (st = build_all_wide()) != JT_OK) return bail(st);
     std::vector<DInstTrav> itrav(scene->ninstances);
     std::vector<int4> iblas(scene->ninstances);
     std::vector<DInstShade> ishade(scene->ninstances);
@@ -981,6 +984,17 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         }
         c->lds_scene_bytes = S.blob_n16 ? bytes : 0;
     }
+    if (params->traversal == JT_TRAVERSAL_AUTO && !S.blob_n16) {
+        // HBM mode: the wide records (the binary nodes stay uploaded, unused); the instances'
+        // BLAS roots become root records
+        if ((st = build_all_wide()) != JT_OK) return bail(st);
+        for (int k0 = 0; k0 < scene->ninstances; k0++) iblas[inst_new[k0]].x = wroot[scene->instances[k0].shape];
+        if ((st = upload(c, wnodes, &S.wnodes)) || (st = upload(c, iblas, &S.inst_blas))) return bail(st);
+        S.tlas_wnodes = tlas_wnodes;
+        c->wide = true;
+    }
+    c->traversal = params->traversal == JT_TRAVERSAL_AUTO ? (c->wide ? JT_TRAVERSAL_WIDE : JT_TRAVERSAL_NEAR)
+                                                          : params->traversal;
     S.ovf = nullptr;
     S.ovf_stride = 0;
     S.ring = c->ring;
@@ -1548,12 +1562,15 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     char tmp[640];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d,%d,%s> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d env_alias=%d light_inline=%d%s",
+                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d env_alias=%d light_inline=%d "
+                  "traversal=%s%s",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, c->kmask, c->wide ? "true" : "false",
                   c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
                   c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->P.nct, c->tiles, BLOCK,
-                  c->env_alias ? 1 : 0, c->S.light_inline, filt);
+                  c->env_alias ? 1 : 0, c->S.light_inline,
+                  c->traversal == JT_TRAVERSAL_REFERENCE ? "reference" : c->traversal == JT_TRAVERSAL_NEAR ? "near" : "wide",
+                  filt);
     std::snprintf(buf, (size_t)n, "%s", tmp);
     return JT_OK;
 }

@@ -33,7 +33,7 @@ STATUS_NAMES = {
 MATERIAL_TYPES = ["matte", "glossy", "reflective", "transparent", "refractive", "subsurface",
                   "volumetric", "gltfpbr"]
 # jt_traversal: BVH child visit order (include/jtrace.h)
-TRAVERSAL_ORDERS = ["reference", "near", "wide"]
+TRAVERSAL_ORDERS = ["reference", "near", "wide", "auto"]
 
 f32p = C.POINTER(C.c_float)
 i32p = C.POINTER(C.c_int32)

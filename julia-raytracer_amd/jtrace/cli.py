@@ -56,7 +56,7 @@ def _parser() -> argparse.ArgumentParser:
                    help="GPUs of this node to shard every batch over, devices 0..N-1 (extension)")
     p.add_argument("--missing", choices=["error", "drop"], default="error",
                    help="missing scene assets: error (reference) or drop (extension)")
-    p.add_argument("--traversal", choices=["reference", "near", "wide"], default=DEFAULT_TRAVERSAL,
+    p.add_argument("--traversal", choices=["reference", "near", "wide", "auto"], default=DEFAULT_TRAVERSAL,
                    help="BVH child order: the near child first (default), or the reference's far-first "
                         "order (extension; the images differ only where two hits tie at exactly equal t)")
     return p

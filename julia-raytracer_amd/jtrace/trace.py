@@ -151,9 +151,18 @@ class TraceState:
 
     def describe(self) -> str:
         """Launch configuration of the next trace_range (kernel instance, scene mode, grid)."""
-        buf = C.create_string_buffer(512)
-        abi.check(self.lib, self.lib.jt_describe(self.handle, buf, 512))
+        buf = C.create_string_buffer(1024)
+        abi.check(self.lib, self.lib.jt_describe(self.handle, buf, 1024))
         return buf.value.decode()
+
+    @property
+    def traversal(self) -> str:
+        """The BVH traversal this context runs ("reference", "near" or "wide"): jt_params.traversal,
+        with "auto" resolved by the library (near when the scene runs from LDS, wide otherwise)."""
+        for tok in self.describe().split():
+            if tok.startswith("traversal="):
+                return tok.split("=", 1)[1]
+        raise RuntimeError("jt_describe reports no traversal")
 
     def reset(self):
         abi.check(self.lib, self.lib.jt_reset(self.handle))

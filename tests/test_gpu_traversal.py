@@ -82,3 +82,29 @@ def test_near_order_rejects_bad_value(gpu, abi, lib, cornell_abi):
     with pytest.raises(abi.JTError) as e:
         trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
     assert e.value.status == -1
+
+
+@pytest.mark.parametrize("name,expect", [("cornellbox", "near"), ("bathroom1", "wide")])
+def test_auto_traversal_resolves_by_scene_mode(gpu, abi, lib, oracle, cornell_abi, name, expect):
+    """JT_TRAVERSAL_AUTO: near for a scene that runs from LDS (cornellbox), wide for one in HBM
+    mode (bathroom1); the render equals the explicit order's bit for bit and meets the parity bar
+    against the oracle's restatement of that order."""
+    from jtrace import trace
+    sa = cornell_abi if name == "cornellbox" else scene_abi(name)
+    bvh = trace.make_scene_bvh(sa, False, lib)
+    lights = trace.make_trace_lights(sa, lib)
+    out = {}
+    for order in ("auto", expect):
+        p = make_params(abi, resolution=96, samples=2, traversal=order)
+        st = trace.make_trace_state(sa, bvh, lights, p, lib)
+        assert st.traversal == expect, st.describe()
+        st.set_counters(1)
+        st.trace_range(0, 2)
+        out[order] = (st.get_image(), st.counters())
+        st.close()
+    assert np.array_equal(out["auto"][0], out[expect][0])
+    assert out["auto"][1]["nodes"] == out[expect][1]["nodes"]
+    p = make_params(abi, resolution=96, samples=2, traversal=expect)
+    g = render_gpu(lib, sa, p, 0, 2)
+    o = render_oracle(oracle, sa, p, g[0].shape[1], g[0].shape[0], 0, 2)
+    check_parity(g, o, f"{name}/auto->{expect}")

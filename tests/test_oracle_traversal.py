@@ -49,5 +49,6 @@ def test_params_carry_the_traversal_order(abi):
     assert make_params(abi, traversal="near").traversal == 1
     assert make_params(abi, traversal="reference").traversal == 0
     assert make_params(abi, traversal="wide").traversal == 2
+    assert make_params(abi, traversal="auto").traversal == 3
     assert abi.jt_params().traversal == 0  # the C-ABI zero value is the reference's order
     assert abi.jt_params.traversal.offset == 64 and abi.C.sizeof(abi.jt_params) == 72
