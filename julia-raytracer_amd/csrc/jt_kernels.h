@@ -680,6 +680,25 @@ __device__ __forceinline__ void wide_box(const float4& r0, const uint4& r1, cons
     a = make_float4(deq(r0.x, r1.x, sh, sx), deq(r0.x, r1.y, sh, sx), deq(r0.y, r1.z, sh, sy), deq(r0.y, r1.w, sh, sy));
     b = make_float4(deq(r0.z, r2.x, sh, sz), deq(r0.z, r2.y, sh, sz), 0.0f, 0.0f);
 }
+#ifndef JT_WIDE_PK
+#define JT_WIDE_PK 1
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
+// (lo - o) * dinv, (hi - o) * dinv of one axis of a dequantised box: lo / hi = origin + byte * scale
+// (exact product, one rounding: fma), then the reference's slab products (src/geometry.jl:96-105)
+__device__ __forceinline__ f2v slab_pair(unsigned wlo, unsigned whi, int sh, float s, float origin, float o, float dinv) {
+    const f2v q = {(float)((wlo >> sh) & 255u), (float)((whi >> sh) & 255u)};
+    const f2v b = __builtin_elementwise_fma(q, (f2v){s, s}, (f2v){origin, origin});
+    return (b - (f2v){o, o}) * (f2v){dinv, dinv};
+}
+// intersect_bbox's decision from the six slab values (mx, Mx, my, My, mz, Mz), as intersect_bbox
+__device__ __forceinline__ bool slab_test(float mx, float Mx, float my, float My, float mz, float Mz, float tmin, float tmax) {
+    const bool nan = __builtin_isnan(mx) | __builtin_isnan(my) | __builtin_isnan(mz) | __builtin_isnan(Mx) |
+                     __builtin_isnan(My) | __builtin_isnan(Mz);
+    const float t0 = vmax3(vmin(mx, Mx), vmin(my, My), vmax(vmin(mz, Mz), tmin));
+    const float t1 = vmin3(vmax(mx, Mx), vmax(my, My), vmin(vmax(mz, Mz), tmax));
+    return !nan && slab_pass(t0, t1);
+}
 // Stack entries of the wide traversal (32 bits): a group — the children of record `index` still
 // to visit (bit 31 clear; bits 28-30 the record's flips for this ray, 24-27 the visit-order mask
 // of children whose boxes passed, 0-23 the record) — or an instance range (bit 31 set; bits 24-25
@@ -708,9 +727,20 @@ __device__ __forceinline__ void wide_visit(const DScene& S, Trav& T, int* stack,
     unsigned hits = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
+#if JT_WIDE_PK
+        // the reference's slab test on the dequantised box, each axis's two planes as one packed
+        // pair (v_pk_fma / v_pk_add / v_pk_mul: the same IEEE operations, half the instructions)
+        const int sh = 8 * c;
+        const f2v tx = slab_pair(r1.x, r1.y, sh, sx, r0.x, T.lo.x, T.ldinv.x);
+        const f2v ty = slab_pair(r1.z, r1.w, sh, sy, r0.y, T.lo.y, T.ldinv.y);
+        const f2v tz = slab_pair(r2.x, r2.y, sh, sz, r0.z, T.lo.z, T.ldinv.z);
+        const bool pass = slab_test(tx.x, tx.y, ty.x, ty.y, tz.x, tz.y, ray_eps, T.tmax);
+#else
         float4 a, b;
         wide_box(r0, r1, r2, sx, sy, sz, c, a, b);
-        if (wide_word(r3, c) != W_EMPTY && intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, a, b)) hits |= 1u << c;
+        const bool pass = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, a, b);
+#endif
+        if (wide_word(r3, c) != W_EMPTY && pass) hits |= 1u << c;
     }
     if (!hits) return;
     const unsigned ax = meta >> 24;

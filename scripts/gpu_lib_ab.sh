@@ -17,7 +17,7 @@ for rep in 1 2; do
   for sc in $SCENES; do
     for lib in "$@"; do
       if [ "$lib" = base ]; then L=julia-raytracer_amd/build/libjtrace_hip.so; else L=julia-raytracer_amd/build/libjtrace_hip_$lib.so; fi
-      JTRACE_LIB=$L scripts/gpu_step.sh 240 $O/${sc}_${lib}_$rep.log timeout -k 10 220 python bench.py --no-cpu-baseline --no-reference-order --steps 2 --warmup 1 $(args $sc) || exit 1
+      JTRACE_LIB=$L scripts/gpu_step.sh 240 $O/${sc}_${lib}_$rep.log timeout -k 10 220 python bench.py --no-cpu-baseline --no-reference-order --steps 2 --warmup 1 $(args $sc) ${AB_ARGS:-} || exit 1
       echo "$sc $lib rep$rep => $(grep -h '"value"' $O/${sc}_${lib}_$rep.log | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print(round(d["value"],1))')" | tee -a $O/summary.txt
     done
   done

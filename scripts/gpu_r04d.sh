@@ -9,6 +9,7 @@ scripts/gpu_step.sh 600 $O/pytest.log python -u -m pytest tests -x -v -m gpu -rf
 tail -2 $O/pytest.log
 grep -q " failed\| error" $O/pytest.log && { echo "GPU tests failed: stopping"; exit 1; }
 bash scripts/gpu_wide.sh $1/wide skip-tests || exit 1
+AB_SCENES="b1 ec" AB_ARGS="--traversal wide" bash scripts/gpu_lib_ab.sh $1/abpk base nopk || exit 1
 scripts/gpu_step.sh 300 $O/signature.log python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-reference-order --write-signature || exit 1
 cp profiles/image_signatures.json $O/ || exit 1
 scripts/gpu_step.sh 400 $O/bench.log python bench.py || exit 1
