@@ -2215,6 +2215,47 @@ void or_free_lights(jt_lights* lights) {
 }
 
 /* ============================================================== KAT entry points */
+/* Property check of the wide records (JT_TRAVERSAL_WIDE) of every tree of a scene BVH, for the
+ * tests: out[0] records, out[1] children whose dequantised box does NOT contain the exact box
+ * (must be 0: the quantisation is conservative), out[2] leaves reached (must equal the binary
+ * trees' leaves), out[3] the mean dequantised/exact volume ratio x 1000 over children with a
+ * non-degenerate box (how loose the bytes make the boxes). */
+static void w_check_tree(const jt_bvh_tree* b, const wtree_t* t, int64_t* out, double* vol, int64_t* nvol) {
+    for (int r = 0; r < t->n; r++) {
+        const wrec_t* w = &t->r[r];
+        out[0]++;
+        for (int k = 0; k < 4; k++) {
+            if (w->child[k] < 0) continue;
+            const jt_bvh_node* c = &b->nodes[w->child[k]];
+            double ve = 1, vq = 1;
+            for (int ax = 0; ax < 3; ax++) {
+                float lo = w->o[ax] + (float)w->lo[ax][k] * w->s[ax];
+                float hi = w->o[ax] + (float)w->hi[ax][k] * w->s[ax];
+                if (!(lo <= c->bmin[ax] && hi >= c->bmax[ax])) out[1]++;
+                ve *= (double)c->bmax[ax] - (double)c->bmin[ax];
+                vq *= (double)hi - (double)lo;
+            }
+            if (!c->internal) out[2]++;
+            if (ve > 0) { *vol += vq / ve; (*nvol)++; }
+        }
+    }
+}
+int or_wide_check(const jt_bvh_tree* tlas, const jt_bvh_tree* blas, int32_t nblas, int64_t* out) {
+    double vol = 0;
+    int64_t nvol = 0;
+    out[0] = out[1] = out[2] = out[3] = 0;
+    for (int i = -1; i < nblas; i++) {
+        const jt_bvh_tree* b = i < 0 ? tlas : &blas[i];
+        if (b->nnodes == 0) continue;
+        wtree_t t = {0, 0, NULL};
+        if (w_build(b, 0, &t) < 0) { free(t.r); return JT_ERR_UNSUPPORTED; }
+        w_check_tree(b, &t, out, &vol, &nvol);
+        free(t.r);
+    }
+    out[3] = nvol ? (int64_t)(1000.0 * vol / (double)nvol) : 0;
+    return JT_OK;
+}
+
 int or_intersect_triangle(const float* o, const float* d, float tmin, float tmax, const float* p1, const float* p2,
                           const float* p3, float* out_uvt) {
     ray3 r = {V3(o[0], o[1], o[2]), V3(d[0], d[1], d[2]), tmin, tmax};

@@ -56,6 +56,8 @@ float or_fresnel_dielectric(float eta, const float* normal, const float* outgoin
 void or_rng_first(uint64_t seed, int32_t pixel, int32_t sample, int32_t n, float* out);
 void or_inverse_frame(const float* frame, int32_t non_rigid, float* out);
 void or_srgb_to_rgb(const uint8_t* bytes, int32_t n, float* out);
+/* wide-record property check (tests): records, non-conservative children, leaves, volume ratio x 1000 */
+int or_wide_check(const jt_bvh_tree* tlas, const jt_bvh_tree* blas, int32_t nblas, int64_t* out);
 
 #ifdef __cplusplus
 }

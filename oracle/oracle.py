@@ -45,6 +45,8 @@ def _load(abi):
     lib.or_inverse_frame.restype = None
     lib.or_srgb_to_rgb.argtypes = [C.POINTER(C.c_uint8), C.c_int32, f32p]
     lib.or_srgb_to_rgb.restype = None
+    lib.or_wide_check.argtypes = [C.POINTER(abi.jt_bvh_tree), C.POINTER(abi.jt_bvh_tree), C.c_int32,
+                                  C.POINTER(C.c_int64)]
     return lib
 
 
@@ -75,6 +77,16 @@ class Oracle:
         if st != 0:
             raise RuntimeError(f"oracle lights failed: {st}")
         return _Owned(out, self.lib.or_free_lights)
+
+    def wide_check(self, bvh):
+        """The wide records of every tree of `bvh` (JT_TRAVERSAL_WIDE): dict of records,
+        non-conservative children (must be 0), leaves, mean dequantised/exact box volume ratio."""
+        out = (C.c_int64 * 4)()
+        b = bvh.struct
+        st = self.lib.or_wide_check(C.byref(b.tlas), b.blas, b.nshapes, out)
+        if st != 0:
+            raise RuntimeError(f"oracle wide check failed: {st}")
+        return {"records": out[0], "violations": out[1], "leaves": out[2], "volume_ratio": out[3] / 1000.0}
 
     def trace(self, scene_abi, bvh, lights, params, width, height, s0, s1, first=0, rows=None,
               nthreads=None, state=None):

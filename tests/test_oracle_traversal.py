@@ -1,6 +1,7 @@
 """The oracle's near-child-first switch (jt_params.traversal, include/jtrace.h) on the CPU: the
 same closest hits up to exact-t ties, fewer nodes popped (src/bvh.jl:331-341 is far-first)."""
 import numpy as np
+import pytest
 
 from conftest import compare_images, make_params
 
@@ -52,3 +53,25 @@ def test_params_carry_the_traversal_order(abi):
     assert make_params(abi, traversal="auto").traversal == 3
     assert abi.jt_params().traversal == 0  # the C-ABI zero value is the reference's order
     assert abi.jt_params.traversal.offset == 64 and abi.C.sizeof(abi.jt_params) == 72
+
+
+@pytest.mark.parametrize("name", ["cornellbox", "features2", "bathroom1", "ecosys"])
+def test_wide_records_are_conservative(abi, oracle, name):
+    """The wide records' quantised child boxes (JT_TRAVERSAL_WIDE, restated in oracle/jt_oracle.c
+    w_build from the product's specification) contain every exact child box on every axis, and
+    every binary leaf is reached; the bytes loosen the boxes by a bounded factor."""
+    from conftest import CORNELL, ROOT
+    from jtrace import sceneio
+    import warnings
+    path = CORNELL if name == "cornellbox" else str(ROOT / "assets" / "scenes" / name / f"{name}.json")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        sa = abi.SceneABI(sceneio.load_scene(path, missing="drop"))
+    bvh = oracle.build_bvh(sa)
+    leaves = sum(1 for t in [bvh.struct.tlas] + [bvh.struct.blas[i] for i in range(bvh.struct.nshapes)]
+                 for k in range(t.nnodes) if not t.nodes[k].internal)
+    c = oracle.wide_check(bvh)
+    print(name, c, "binary leaves", leaves)
+    assert c["violations"] == 0
+    assert c["leaves"] == leaves
+    assert 1.0 <= c["volume_ratio"] < 2.0
