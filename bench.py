@@ -60,6 +60,13 @@ def shade_record_bytes(scene) -> int:
     return best
 
 
+def library_build_hash(lib) -> str:
+    """The source hash embedded in the loaded library (jt_version: "..., source <hash>)")."""
+    import re
+    m = re.search(r"source ([0-9a-f]{16}|unknown)\)", lib.jt_version().decode())
+    return m.group(1) if m else "unknown"
+
+
 def roofline_record(workload: str, kernel: str, build: str):
     """The committed roofline record (profiles/*_roofline/*.json, written on the GPU box by
     scripts/roofline.py from rocprofv3 kernel-trace + PMC passes of this same bench command) for
@@ -184,6 +191,7 @@ def main():
         state = trace.make_trace_state(sa, bvh, lights, jp, lib)
         abi.set_option(lib, "tile_share", None)
 
+    traversal = state.traversal  # "auto" resolved by the library: near from LDS, wide from HBM
     img_t = None
     if world > 1:
         buf = state.device_buffers()
@@ -253,7 +261,7 @@ def main():
     elif rank == 0:
         img_final = (reduced[0].detach().cpu().numpy().reshape(H, W, 4) if world > 1 else state.get_image())
         sig = image_signature(img_final)
-        sig_key = f"{Path(args.scene).stem} {args.sampler} {W}x{H}x{S}spp traversal={args.traversal}" + \
+        sig_key = f"{Path(args.scene).stem} {args.sampler} {W}x{H}x{S}spp traversal={traversal}" + \
             (" bvh=sah" if args.highqualitybvh else "")
         ref_sig = load_signature(SIGNATURES, sig_key)
         if args.write_signature and world == 1:
@@ -326,14 +334,17 @@ def main():
         avg_launch_s = kernel_ms / launches / 1e3
         per_launch = {k: v / max(1, full["launches"]) for k, v in full.items()}  # one step's launches
         logical = algorithmic_bytes(per_launch, shade_record_bytes(scene),
-                                    any(len(s.quads) for s in scene.shapes), args.traversal == "wide")
+                                    any(len(s.quads) for s in scene.shapes), traversal == "wide")
         workload = f"{name} {args.sampler} {W}x{H} {s1 - s0} samples/launch" + \
             (f" tiles 1/{groups}" if groups > 1 else "") + \
-            ("" if args.traversal == "reference" else f" traversal={args.traversal}") + \
+            ("" if traversal == "reference" else f" traversal={traversal}") + \
             (" bvh=sah" if args.highqualitybvh else "")
         sys.path.insert(0, str(ROOT / "scripts"))
-        from roofline import VMEM_PEAK_GIPS, source_hash
-        build = source_hash()
+        from roofline import VMEM_PEAK_GIPS
+        # the source hash the Makefile embedded in the library that ran (jt_version), not a hash of
+        # this tree: no compiler is invoked at run time (under a PMC profiler a child process that
+        # execs would be refused), and a record can only match the binary it describes
+        build = library_build_hash(lib)
         rec, rec_src = roofline_record(workload, kernel, build)
         # The roof that binds, from the PMC counts of this kernel on this workload and build
         # (committed record) over THIS run's launch time (HIP events):
@@ -389,7 +400,8 @@ def main():
                        "split": {"tile_groups": groups, "sample_ranges": world // groups,
                                  "rank0_share": {"tiles": share or "all", "samples": [s0, s1]}},
                        "sampler": args.sampler, "width": W, "height": H, "spp": S, "bounces": 8,
-                       "traversal": args.traversal, "bvh": "sah" if args.highqualitybvh else "middle",
+                       "traversal": traversal, "traversal_requested": args.traversal,
+                       "bvh": "sah" if args.highqualitybvh else "middle",
                        "parallelism": f"{groups} tile groups x {world // groups} sample ranges + RCCL reduce"},
             "render_s": round(ms_per_step / 1e3, 4),
             "msamples_per_s": round((agg["paths"] if partial else W * H * S * args.steps) / elapsed / 1e6, 2),

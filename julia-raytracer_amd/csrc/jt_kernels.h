@@ -680,8 +680,9 @@ __device__ __forceinline__ void wide_box(const float4& r0, const uint4& r1, cons
     a = make_float4(deq(r0.x, r1.x, sh, sx), deq(r0.x, r1.y, sh, sx), deq(r0.y, r1.z, sh, sy), deq(r0.y, r1.w, sh, sy));
     b = make_float4(deq(r0.z, r2.x, sh, sz), deq(r0.z, r2.y, sh, sz), 0.0f, 0.0f);
 }
+// packed slab pairs in the wide visit: measured slower (bathroom1 -3 %, ecosys -2 %; gpurun_out/r04d/abpk)
 #ifndef JT_WIDE_PK
-#define JT_WIDE_PK 1
+#define JT_WIDE_PK 0
 #endif
 typedef float f2v __attribute__((ext_vector_type(2)));
 // (lo - o) * dinv, (hi - o) * dinv of one axis of a dequantised box: lo / hi = origin + byte * scale

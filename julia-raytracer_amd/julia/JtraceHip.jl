@@ -180,10 +180,11 @@ end
 # Params src/cli.jl:90-138: camera is find_camera's 1-based index (src/jtrace.jl:61), sampler is
 # already the 1-based index into SAMPLER_TYPES = ["path", "naive"] (src/cli.jl:88,111-116) —
 # the C side's jt_sampler uses the same numbering — and clamp is an Int (src/cli.jl:105)
-# traversal: 1 = near child first (jt_traversal, the product default: the reference's far-first
-# order, src/bvh.jl:331-341, is performance-only; only exact-t ties resolve differently), 0 = the
-# reference's order
-pack_params(p::Params; device = 0, seed = 0x5EED, traversal = 1) =
+# traversal (jt_traversal): 3 = auto, the product default (the binary tree near child first for a
+# scene that runs from LDS, the 4-wide quantised records otherwise), 1 = near, 2 = wide, 0 = the
+# reference's far-first order (src/bvh.jl:331-341); they differ only where two hits tie at exactly
+# equal t or a box is culled by the slab test's rounding
+pack_params(p::Params; device = 0, seed = 0x5EED, traversal = 3) =
     JtParams(Int32(p.camera - 1), Int32(p.resolution), Int32(0), Int32(0), Int32(p.samples), Int32(p.bounces),
              Int32(p.sampler), Int32(p.clamp), Int32(p.envhidden), Int32(p.tentfilter), Int32(p.nocaustics),
              Int32(p.batch), Int32(p.bvhstacksize), Int32(device), UInt64(seed), Int32(traversal))

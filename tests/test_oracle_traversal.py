@@ -43,10 +43,11 @@ def test_oracle_wide_matches_binary_orders(abi, oracle, cornell_abi):
 
 def test_params_carry_the_traversal_order(abi):
     from jtrace.cli import DEFAULT_TRAVERSAL, Params, parse_cli_args
-    # one default for the parser, the dataclass and make_params: near first (the benched order)
-    assert DEFAULT_TRAVERSAL == "near"
+    # one default for the parser, the dataclass and abi.make_params: auto (resolved by the library)
+    assert DEFAULT_TRAVERSAL == "auto"
     assert Params(scene="x").traversal == parse_cli_args(["--scene", "x"]).traversal == DEFAULT_TRAVERSAL
-    assert make_params(abi).traversal == 1
+    assert abi.make_params(Params(scene="x"), 0).traversal == 3
+    assert make_params(abi).traversal == 1  # the tests' own default: near, restated by the oracle
     assert make_params(abi, traversal="near").traversal == 1
     assert make_params(abi, traversal="reference").traversal == 0
     assert make_params(abi, traversal="wide").traversal == 2
