@@ -315,7 +315,10 @@ def main():
     # two cameras and framings — are checked to agree (a libm ulp may flip a rare path: <= 0.1 %)
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1 and not partial:
-        cpu = cpu_baseline(sa, jp, W, H, args.cpu_threads, args.cpu_spp, args.highqualitybvh)
+        # the oracle runs the order the GPU resolved "auto" to (it has no LDS/HBM mode to choose by)
+        jp_cpu = type(jp).from_buffer_copy(jp)
+        jp_cpu.traversal = abi.TRAVERSAL_ORDERS.index(traversal)
+        cpu = cpu_baseline(sa, jp_cpu, W, H, args.cpu_threads, args.cpu_spp, args.highqualitybvh)
         state.reset()
         state.trace_range(0, args.cpu_spp)
         g = state.counters()

@@ -396,13 +396,23 @@ __device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T
 // A lane's next step in either traversal: a primitive test (nprim > 0) or a node step (a stack
 // entry, or in the wide traversal a pending child word); neither: its query is done (sp 0) or the
 // lane has no samples left (sp < 0).
+// JT_BIN_NXT: the binary traversal keeps the entry it pops next in a register (Trav::nxt) instead
+// of pushing it and popping it back: an internal node pushes only its second child, a TLAS leaf all
+// but its first instance. The same entries in the same order (results and counters unchanged; the
+// GPU suite passed on it), one LDS write and one dependent LDS read fewer per internal node — but
+// measured slower where the binary order runs in production: cornellbox 9922/9907 vs 10027/9981
+// Mrays/s without it (-0.9 %); near order in HBM mode features2 and bathroom1 within +-1 %
+// (gpurun_out/r04g/ab_cb, ab_near). Off.
+#ifndef JT_BIN_NXT
+#define JT_BIN_NXT 0
+#endif
 template <bool WIDE>
 __device__ __forceinline__ bool wants_node(const Trav& T) {
-    return T.nprim == 0 && (T.sp > 0 || (WIDE && T.nxt != W_EMPTY));
+    return T.nprim == 0 && (T.sp > 0 || ((WIDE || JT_BIN_NXT) && T.nxt != W_EMPTY));
 }
 template <bool WIDE>
 __device__ __forceinline__ bool query_done(const Trav& T) {
-    return (T.sp | T.nprim) == 0 && (!WIDE || T.nxt == W_EMPTY);
+    return (T.sp | T.nprim) == 0 && (!(WIDE || JT_BIN_NXT) || T.nxt == W_EMPTY);
 }
 
 __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d, unsigned root, int* stack) {
@@ -424,10 +434,15 @@ __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d
     T.cur_kind = KIND_TRI;
     T.inst_space = 0;
     T.negmask = neg_mask(d, S.order_flip);
-    stack[0] = (int)root;
-    T.sp = 1;
     T.low = 0;
-    T.nxt = W_EMPTY;
+    if (JT_BIN_NXT) {
+        T.sp = 0;
+        T.nxt = root;
+    } else {
+        stack[0] = (int)root;
+        T.sp = 1;
+        T.nxt = W_EMPTY;
+    }
 }
 // query_begin of the wide traversal: the root is the first node step's child word (the TLAS
 // root record, or an instance leaf of one instance for intersect_instance_bvh); the stack is empty
@@ -566,7 +581,16 @@ template <int RING, bool OVF, int COUNT, bool NCACHE, int F>
 __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
     // without FT_XFORM every instance ray is the world ray: no transform, no space switch
     constexpr bool XF = (F & FT_XFORM) != 0;
-    const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
+    unsigned e;
+    if (JT_BIN_NXT) {  // the pending entry, else the stack's top
+        const bool held = T.nxt != W_EMPTY;
+        unsigned p = 0;
+        if (!held) p = st_pop<RING, OVF>(S, T, stack, pixel);
+        e = held ? T.nxt : p;
+        T.nxt = W_EMPTY;
+    } else {
+        e = st_pop<RING, OVF>(S, T, stack, pixel);
+    }
     unsigned type = e >> 30, idx = e & IDX_MASK;
     if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
         if (COUNT) cnt.instances++;
@@ -639,15 +663,22 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             const bool k1 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n1.a, n1.b);
             if (COUNT) cnt.nodes += (k0 ? 0 : 1) + (k1 ? 0 : 1);
             const unsigned ptag = type << 30 | (unsigned)T.nh << 24;  // pre-tested at hit count nh
-            if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_second);
-            if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_first);
+            if (JT_BIN_NXT) {  // the child popped next stays in nxt
+                if (k0 && k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_second);
+                if (k0 || k1) T.nxt = ptag | (k1 ? c_first : c_second);
+            } else {
+                if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_second);
+                if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_first);
+            }
         } else {
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_second);
-            st_push<RING, OVF>(S, T, stack, pixel, tag | c_first);
+            if (JT_BIN_NXT) T.nxt = tag | c_first;
+            else st_push<RING, OVF>(S, T, stack, pixel, tag | c_first);
         }
     } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
-        for (int k = num - 1; k >= 0; k--)
+        for (int k = num - 1; k >= (JT_BIN_NXT ? 1 : 0); k--)
             st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | SNAP_NONE | (unsigned)(start + k));
+        if (JT_BIN_NXT && num > 0) T.nxt = (T_INST << 30) | SNAP_NONE | (unsigned)start;
     } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
@@ -906,7 +937,15 @@ constexpr unsigned CTL_BOUNCE = 0x7fffu, CTL_OPB = 15, CTL_FLAGS = 23, CTL_LC = 
 #ifndef JT_PARK_PB
 #define JT_PARK_PB 1
 #endif
-constexpr int PARK_SLOTS = 7 + (JT_PARK_PB ? 1 : 0);  // radiance xyz, max_roughness, lq xyz, pb
+// weight (the path throughput) is read and written only in the shading code as well; parked in
+// slots [8, 11) it frees three registers across the traversal loop (JT_PARK_W): features2's kernel
+// then spills nothing (3 VGPRs and 2 in-loop scratch stores per shade without it), but its 43 KiB
+// of LDS per workgroup fit only 3 workgroups per CU instead of 4: features2 -12 %, bathroom1 -14 %,
+// ecosys -13 %, and as much at 3 waves with 168 VGPRs (gpurun_out/r04g/ab_parkw). Off.
+#ifndef JT_PARK_W
+#define JT_PARK_W 0
+#endif
+constexpr int PARK_SLOTS = 7 + (JT_PARK_PB ? 1 : 0) + (JT_PARK_PB && JT_PARK_W ? 3 : 0);  // radiance xyz, max_roughness, lq xyz, pb, weight xyz
 // slots: [0, 3) radiance, 3 max_roughness, [4, 7) lq, 7 pb. The mesh kernels park (features2 +6 %,
 // bathroom1 +14 %, ecosys +9 %: their spills fell from 12-28 to 0-7 VGPRs). The FT_NONE kernel
 // (cornellbox, 2-8 spilled VGPRs either way) does not: its light-hit steps read the light-chain
@@ -916,7 +955,7 @@ __host__ __device__ constexpr bool park_lq(int F) { return park(F); }
 __host__ __device__ constexpr int park_slots(int F) { return park(F) ? PARK_SLOTS : 0; }
 struct Path {
     v3 o, d;                    // pending ray (during PH_LIGHT the light query's: origin / incoming)
-    v3 radiance_, weight;  // during PH_LIGHT weight already holds weight .* f (src/trace.jl:386)
+    v3 radiance_, weight_;  // during PH_LIGHT weight already holds weight .* f (src/trace.jl:386)
     Rng rng;
     unsigned ctl;  // bounce | opbounce | flags | lcount (CTL_*)
     int phase;
@@ -964,6 +1003,20 @@ struct Path {
         if (park(F) && JT_PARK_PB) pk[7 * BLOCK] = v;
         else pb_ = v;
     }
+    template <int F>
+    __device__ __forceinline__ v3 weight() const {
+        return park(F) && JT_PARK_PB && JT_PARK_W ? V3(pk[8 * BLOCK], pk[9 * BLOCK], pk[10 * BLOCK]) : weight_;
+    }
+    template <int F>
+    __device__ __forceinline__ void set_weight(v3 v) {
+        if (park(F) && JT_PARK_PB && JT_PARK_W) {
+            pk[8 * BLOCK] = v.x;
+            pk[9 * BLOCK] = v.y;
+            pk[10 * BLOCK] = v.z;
+        } else {
+            weight_ = v;
+        }
+    }
     __device__ __forceinline__ int bounce() const { return (int)(ctl & CTL_BOUNCE); }
     __device__ __forceinline__ int opbounce() const { return (int)((ctl >> CTL_OPB) & 0xffu); }
     __device__ __forceinline__ bool flag(int f) const { return (ctl >> CTL_FLAGS) & (unsigned)f; }
@@ -992,12 +1045,13 @@ __device__ __forceinline__ bool next_bounce_retry(const DParams& P, Path& st) {
     return false;
 }
 // end of a bounce: weight checks and Russian roulette (src/trace.jl:455-465, 557-567)
+template <int F>
 __device__ __forceinline__ bool after_weight(const DParams& P, Path& st) {
-    if (is_zero(st.weight) || !all_finite(st.weight)) return true;
+    if (is_zero(st.weight<F>()) || !all_finite(st.weight<F>())) return true;
     if (st.bounce() > 3) {
-        float rr_prob = jl_min(0.99f, max3(st.weight));
+        float rr_prob = jl_min(0.99f, max3(st.weight<F>()));
         if (rand1f(st.rng) >= rr_prob) return true;
-        st.weight = st.weight * (1 / rr_prob);
+        st.set_weight<F>(st.weight<F>() * (1 / rr_prob));
     }
     return next_bounce(P, st);
 }
@@ -1010,8 +1064,8 @@ __device__ __forceinline__ bool light_advance(const DScene& S, const DParams& P,
         if (st.li >= S.nlights) {
             st.o = st.lq<F>();  // the next bounce's ray starts at the shading position
             const float pdf = st.pdf * S.light_pick_pdf;  // sample_uniform_pdf(nlights), host-computed
-            st.weight = st.weight / (0.5f * st.pb<F>() + 0.5f * pdf);  // (weight .* f) / (...)
-            return after_weight(P, st);
+            st.set_weight<F>(st.weight<F>() / (0.5f * st.pb<F>() + 0.5f * pdf));  // (weight .* f) / (...)
+            return after_weight<F>(P, st);
         }
         const DLight l = S.lights[st.li];
         if (!(F & FT_NOIL) && l.instance >= 0) {
@@ -1141,7 +1195,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
                                          unsigned& shades) {
     if (!isec.hit) {
         if (st.bounce() > 0 || !P.envhidden)
-            st.set_radiance<F>(st.radiance<F>() + st.weight * eval_environment<F>(S, st.d));
+            st.set_radiance<F>(st.radiance<F>() + st.weight<F>() * eval_environment<F>(S, st.d));
         return true;
     }
     bool in_volume = false;
@@ -1150,7 +1204,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
         float distance = sample_transmittance(st.vol.density, isec.t, rl, rd);
         v3 tr = eval_transmittance(st.vol.density, distance);
         float tp = sample_transmittance_pdf(st.vol.density, distance, isec.t);
-        st.weight = (st.weight * tr) / tp;
+        st.set_weight<F>((st.weight<F>() * tr) / tp);
         in_volume = distance < isec.t;
         isec.t = distance;
     }
@@ -1173,7 +1227,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
             st.set_flag(F_HIT);
             aov_update<F>(aov, sh.mat.color, sh.normal);
         }
-        st.set_radiance<F>(st.radiance<F>() + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0)));
+        st.set_radiance<F>(st.radiance<F>() + st.weight<F>() * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0)));
         v3 incoming;
         const bool delta = is_delta(sh.mat);
         if (!delta) {
@@ -1191,10 +1245,10 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
             v3 fb;
             float pbv;
             eval_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming, fb, pbv);
-            st.weight = st.weight * fb;
+            st.set_weight<F>(st.weight<F>() * fb);
             st.set_pb<F>(pbv);
 #else
-            st.weight = st.weight * eval_bsdfcos<F>(sh.mat, sh.normal, outgoing, incoming);
+            st.set_weight<F>(st.weight<F>() * eval_bsdfcos<F>(sh.mat, sh.normal, outgoing, incoming));
             st.set_pb<F>(sample_bsdfcos_pdf<F>(sh.mat, sh.normal, outgoing, incoming));
 #endif
         } else {
@@ -1202,7 +1256,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
             incoming = sample_delta<F>(sh.mat, sh.normal, outgoing, rnl);
             v3 f = eval_delta<F>(sh.mat, sh.normal, outgoing, incoming);
             float pd = sample_delta_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
-            st.weight = (st.weight * f) / pd;
+            st.set_weight<F>((st.weight<F>() * f) / pd);
         }
         // volume stack push/pop (:405-421); independent of the weight update it follows
         const int mtype = sh.mat.type;
@@ -1219,7 +1273,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
         }
         st.o = sh.position;
         st.d = incoming;
-        return delta ? after_weight(P, st) : begin_light_pdf<F>(S, P, st);
+        return delta ? after_weight<F>(P, st) : begin_light_pdf<F>(S, P, st);
     }
     // volume scattering (:424-453)
     v3 outgoing = -st.d;
@@ -1235,7 +1289,7 @@ __device__ __forceinline__ bool path_hit(const DScene& S, const DParams& P, Path
         incoming = sample_lights<F>(S, position, rl, rel, ruv);
     }
     if (is_zero(incoming)) return true;
-    st.weight = st.weight * eval_scattering(st.vol, outgoing, incoming);
+    st.set_weight<F>(st.weight<F>() * eval_scattering(st.vol, outgoing, incoming));
     st.set_pb<F>(sample_scattering_pdf(st.vol, outgoing, incoming));
     st.o = position;
     st.d = incoming;
@@ -1248,7 +1302,7 @@ __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Pat
                                           unsigned& shades) {
     if (!isec.hit) {
         if (st.bounce() > 0 || !P.envhidden)
-            st.set_radiance<F>(st.radiance<F>() + st.weight * eval_environment<F>(S, st.d));
+            st.set_radiance<F>(st.radiance<F>() + st.weight<F>() * eval_environment<F>(S, st.d));
         return true;
     }
     v3 outgoing = -st.d;
@@ -1265,7 +1319,7 @@ __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Pat
         st.set_flag(F_HIT);
         aov_update<F>(aov, sh.mat.color, sh.normal);
     }
-    st.set_radiance<F>(st.radiance<F>() + st.weight * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0)));
+    st.set_radiance<F>(st.radiance<F>() + st.weight<F>() * (dot(sh.normal, outgoing) >= 0 ? sh.mat.emission : V3(0, 0, 0)));
     v3 incoming, f;
     float p;
     if (sh.mat.roughness != 0) {
@@ -1286,10 +1340,10 @@ __device__ __forceinline__ bool naive_hit(const DScene& S, const DParams& P, Pat
         f = eval_delta<F>(sh.mat, sh.normal, outgoing, incoming);
         p = sample_delta_pdf<F>(sh.mat, sh.normal, outgoing, incoming);
     }
-    st.weight = (st.weight * f) / p;
+    st.set_weight<F>((st.weight<F>() * f) / p);
     st.o = sh.position;
     st.d = incoming;
-    return after_weight(P, st);
+    return after_weight<F>(P, st);
 }
 
 // eval_camera (src/scene.jl:372-411)
@@ -1332,7 +1386,7 @@ __device__ __forceinline__ void start_path(const DParams& P, int i, int j, int p
     }
     eval_camera(P.cam, uv, P.cam.pinhole ? sample_disk_signs(luv) : sample_disk(luv), st.o, st.d);
     st.set_radiance<F>(V3(0, 0, 0));
-    st.weight = V3(1, 1, 1);
+    st.set_weight<F>(V3(1, 1, 1));
     st.set_max_roughness<F>(0.0f);
     st.ctl = 0u;  // bounce 0 (the first loop iteration: -1 + 1; bounces >= 0 always enters), no flags
     st.phase = PH_SCENE;

@@ -1,0 +1,98 @@
+// The vector-memory ceiling for the HBM-mode kernels' own load mix: dependent
+// random gathers, as a BVH walk does, of the record shapes the traversal and shading load —
+//   mode 0: one 16-B row (dwordx4)                    the round-2 ceiling (td_width_bench mode 0)
+//   mode 1: a 64-B wide node record (4 x dwordx4)     node_step_wide
+//   mode 2: an 80-B triangle pair (5 x dwordx4)       prim_step
+//   mode 3: an 8-B texel pair (dwordx2)               eval_texture
+// over working sets from L2-resident (4 MiB per XCD) through MALL (64-256 MiB) to HBM (2 GiB).
+// Every lane walks its own chain (the next record index from the loaded words); all 64 lanes are
+// active (td_lanes_bench: the TD charges per wave-instruction, not per active lane). Prints the
+// wave-instructions per second per (mode, working set); run it under rocprofv3 --pmc
+// TD_TD_BUSY_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE to see TD busy and the L2 hit rate of each
+// dispatch (one dispatch per line, in print order after a warm-up dispatch).
+// build: hipcc --offload-arch=gfx950 -O3 -o build/td_mix_bench scripts/td_mix_bench.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+template <int MODE>
+__global__ __launch_bounds__(256) void chase(const uint4* rec, unsigned n, int steps, unsigned* out) {
+    unsigned i = ((blockIdx.x * 256u + threadIdx.x) * 2654435761u) & (n - 1);  // n: a power of two
+    unsigned acc = 0;
+    for (int s = 0; s < steps; s++) {
+        unsigned v;
+        if (MODE == 0) {
+            const uint4 a = rec[(size_t)i];
+            v = a.x ^ a.y ^ a.z ^ a.w;
+        } else if (MODE == 1) {
+            const uint4* r = rec + 4 * (size_t)i;
+            const uint4 a = r[0], b = r[1], c = r[2], d = r[3];
+            v = a.x ^ b.y ^ c.z ^ d.w ^ a.w ^ b.x ^ c.y ^ d.z;
+        } else if (MODE == 2) {
+            const uint4* r = rec + 5 * (size_t)i;
+            const uint4 a = r[0], b = r[1], c = r[2], d = r[3], e = r[4];
+            v = a.x ^ b.y ^ c.z ^ d.w ^ e.x ^ a.w ^ b.x ^ c.y ^ d.z ^ e.w;
+        } else {
+            const uint2 a = reinterpret_cast<const uint2*>(rec)[(size_t)i];
+            v = a.x ^ a.y;
+        }
+        acc += v;
+        i = (v * 2654435761u + (unsigned)s) & (n - 1);
+    }
+    out[blockIdx.x * 256u + threadIdx.x] = acc;
+}
+
+template <int MODE>
+float run(const uint4* rec, unsigned n, unsigned* out, int blocks, int steps) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a);
+    chase<MODE><<<blocks, 256>>>(rec, n, steps, out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return ms;
+}
+
+__global__ void fill(uint4* p, size_t n16) {
+    for (size_t k = blockIdx.x * 256ull + threadIdx.x; k < n16; k += (size_t)gridDim.x * 256) {
+        unsigned x = (unsigned)k * 2654435761u + 12345u;
+        p[k] = make_uint4(x, x * 1664525u + 1013904223u, x ^ 0x9e3779b9u, x * 22695477u + 1u);
+    }
+}
+
+int main() {
+    const size_t max_bytes = 2ull << 30;  // 2 GiB: the HBM working set
+    uint4* rec;
+    unsigned* out;
+    const int blocks = 256 * 16;  // 16 workgroups (64 waves) per CU: every SIMD's wave slots filled
+    if (hipMalloc(&rec, max_bytes) != hipSuccess || hipMalloc(&out, (size_t)blocks * 256 * 4) != hipSuccess) return 1;
+    fill<<<4096, 256>>>(rec, max_bytes / 16);
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    const size_t sets[4] = {4ull << 20, 64ull << 20, 256ull << 20, 2ull << 30};
+    const char* name[4] = {"16 B row (dwordx4)", "64 B wide node (4 x dwordx4)", "80 B tri pair (5 x dwordx4)",
+                           "8 B texel pair (dwordx2)"};
+    const int insts[4] = {1, 4, 5, 1};
+    const int rec_bytes[4] = {16, 64, 80, 8};
+    run<0>(rec, 1u << 16, out, blocks, 200);  // warm-up dispatch
+    for (int m = 0; m < 4; m++) {
+        for (int w = 0; w < 4; w++) {
+            unsigned n = 1;
+            while ((size_t)(n * 2ull) * rec_bytes[m] <= sets[w]) n *= 2;
+            const int steps = m == 0 || m == 3 ? 20000 : 5000;
+            float ms = m == 0 ? run<0>(rec, n, out, blocks, steps)
+                     : m == 1 ? run<1>(rec, n, out, blocks, steps)
+                     : m == 2 ? run<2>(rec, n, out, blocks, steps)
+                              : run<3>(rec, n, out, blocks, steps);
+            const double waves = (double)blocks * 4 * steps;  // 4 waves per workgroup
+            printf("mode %d %-30s set %5zu MiB  %8.2f ms  %8.2f G wave-instr/s  %8.1f G records/s\n", m, name[m],
+                   ((size_t)n * rec_bytes[m]) >> 20, ms, waves * insts[m] / ms * 1e-6,
+                   waves * 64 / ms * 1e-6);
+        }
+    }
+    return 0;
+}
