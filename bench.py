@@ -5,7 +5,9 @@ A step = one full render of that workload (every pixel x every sample, bounces=8
 seed 0x5EED) with the scene already resident in HBM: each rank traces its contiguous
 sample range [r*S/N, (r+1)*S/N) of all pixels (no data-path collective), then for N > 1 one
 RCCL reduce (sum of sample-weighted running means) gathers the image on rank 0 — the only
-exchange the path has. value = closest-hit scene queries of all ranks / time.
+exchange the path has, pipelined so that a step's reduce runs during the next
+step's launch (the last one finishes inside the timed region). value = closest-hit scene queries
+of all ranks / time.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -177,7 +179,7 @@ def main():
             "lights_s": round(t_lights - t_bvh, 3), "upload_s": round(t_create - t_lights, 3),
             "total_s": round(t_create - t_0, 3)}
     W, H, S = state.width, state.height, args.spp
-    from jtrace.parallel import (compare_signature, image_signature, load_signature, reduce_running_means,
+    from jtrace.parallel import (compare_signature, image_signature, load_signature,
                                  save_signature, split_plan)
     # this rank's share: 1/G of the 8x8 tiles (G = --tile-groups) x a contiguous
     # 1/(N/G) of the samples; G = 1 is the pure sample split
@@ -202,24 +204,48 @@ def main():
         img_t = torch.as_tensor(_CAI(), device=f"cuda:{dev}")
 
     reduced = [None]  # rank 0, N > 1: the last step's reduced image (the image check below)
+    # N > 1: the path's one exchange, the sum of sample-weighted shard means onto rank 0 (RCCL),
+    # pipelined: a step snapshots its weighted shard image into one of two buffers and starts the
+    # reduce asynchronously, so it runs during the next step's launch; a buffer is reused only
+    # after its previous reduce completed, and drain() ends the last one inside the timed region
+    snaps, pending, last = [], [None, None], [0]
+    if world > 1:
+        snaps = [torch.empty(H * W * 4, dtype=torch.float32, device=img_t.device if backend == "nccl" else "cpu")
+                 for _ in range(2)]
 
     def step():
         state.reset()
         state.trace_range(s0, s1)  # returns when the launch has finished (HIP event sync)
-        if world > 1:  # the path's one exchange: sum of sample-weighted shard means (RCCL)
-            reduced[0] = reduce_running_means(img_t if backend == "nccl" else img_t.cpu(), s1 - s0, S, dist, dst=0)
-            # the reduce reads the library's buffer on torch's stream: finish it before the next
+        if world > 1:
+            i = (last[0] + 1) % 2
+            if pending[i] is not None:
+                pending[i].wait()
+            torch.mul(img_t if backend == "nccl" else img_t.cpu(), float(s1 - s0), out=snaps[i])
+            # the snapshot reads the library's buffer on torch's stream: finish it before the next
             # step's jt_reset clears that buffer on the library's stream
-            torch.cuda.synchronize()
+            torch.cuda.current_stream().synchronize()
+            pending[i] = dist.reduce(snaps[i], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+            last[0] = i
         return state.counters()
+
+    def drain():
+        for i in range(len(pending)):
+            if pending[i] is not None:
+                pending[i].wait()
+                pending[i] = None
+        torch.cuda.synchronize()
+        if world > 1 and rank == 0:
+            reduced[0] = snaps[last[0]] / float(S)
 
     for _ in range(args.warmup):
         step()
+    drain()
     # counting pass: the same step with every traversal counter on (level 1); the timed steps
     # run the production kernel (level 0: paths/rays/light queries). The counts are a
     # deterministic function of (seed, samples, BVH); the ray count cross-checks them.
     state.set_counters(1)
     full = step()
+    drain()
     state.set_counters(0)
     desc = state.describe()
     kernel = desc.split()[0].split("=", 1)[1]
@@ -238,7 +264,7 @@ def main():
             agg[k] += c[k]
         kernel_ms += c["kernel_ms"]
         rays += c["rays"]
-    torch.cuda.synchronize()
+    drain()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -343,7 +369,7 @@ def main():
             ("" if traversal == "reference" else f" traversal={traversal}") + \
             (" bvh=sah" if args.highqualitybvh else "")
         sys.path.insert(0, str(ROOT / "scripts"))
-        from roofline import VMEM_PEAK_GIPS
+        from roofline import VMEM_MIX_PEAK_GIPS
         # the source hash the Makefile embedded in the library that ran (jt_version), not a hash of
         # this tree: no compiler is invoked at run time (under a PMC profiler a child process that
         # execs would be refused), and a record can only match the binary it describes
@@ -355,7 +381,9 @@ def main():
         #    achieved = useful FP32 lane-operations per second, peak = the CUs' FP32 lane rate;
         #  - HBM mode (node / primitive records L2-resident): the vector-memory return path (TD) —
         #    achieved = vector-memory read wave-instructions per second, peak = the measured
-        #    dwordx4 gather ceiling (profiles/r02_pair/td_width_bench.log).
+        #    gather ceiling for the traversal's own node records (scripts/td_mix_bench.hip,
+        #    profiles/r04_tdmix/: 64-B wide records 40.6, 16-B binary rows 34.7 G wave-instr/s);
+        #    td_unstalled_frac (TD busy and not waiting on the cache) beside it agrees with frac.
         # HBM itself (measured traffic / 8 TB/s) is reported beside it as hbm_frac.
         lds_mode = "mode=lds" in desc
         roof = {"bound": "valu" if lds_mode else "vmem/TD", "achieved": None, "peak": None,
@@ -368,7 +396,7 @@ def main():
             if lds_mode and "valu_lane_ops" in d:
                 achieved, peak = d["valu_lane_ops"] / avg_launch_s / 1e9, d["valu_peak_gops"]
             elif not lds_mode and "vmem_rd_per_launch" in d:
-                achieved, peak = d["vmem_rd_per_launch"] / avg_launch_s / 1e9, VMEM_PEAK_GIPS
+                achieved, peak = d["vmem_rd_per_launch"] / avg_launch_s / 1e9, VMEM_MIX_PEAK_GIPS[traversal]
             else:
                 achieved = peak = None
             if achieved is not None:
@@ -377,7 +405,8 @@ def main():
             roof.update(traffic=int(traffic), hbm_achieved_gbs=round(traffic / avg_launch_s / 1e9, 1),
                         hbm_frac=round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5))
             roof["binding"] = {k: d[k] for k in ("valu_issue_frac", "lane_util", "fp32_lane_frac", "td_busy_frac",
-                                                 "vmem_frac", "clock_ghz") if k in d}
+                                                 "td_unstalled_frac", "td_tc_stall_frac_of_busy", "l2_hit_rate",
+                                                 "vmem_mix_frac", "clock_ghz") if k in d}
             roof["binding"]["write_bytes_per_launch"] = int(d["write_bytes"])
             roof["binding"]["profiled_launch_ms"] = round(rec["duration_ns"] / 1e6, 3)
         alg_gbs = logical / avg_launch_s / 1e9

@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef JT_CHUNKS_PER_LAUNCH
+#define JT_CHUNKS_PER_LAUNCH 16  // the automatic chunk: a sixteenth of the launch's samples
+#endif
 #ifndef JT_MAX_CHUNKS
 #define JT_MAX_CHUNKS 32
 #endif

@@ -1220,24 +1220,19 @@ namespace {
 // enqueue one launch over global samples [s0, s1) whose running-mean weight is 1/(s - first + 1)
 int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
     c->P.first = first;
-    // Samples per work unit. LDS mode (small scenes): a quarter of the launch within [8, 64].
-    // HBM mode: as long as keeps >= 32 units per resident wave, up to 256 samples — a wave waits
-    // for its slowest lane at the end of every unit, and a longer unit makes that tail a smaller
-    // share (measured at the configs' own spp: bathroom1 1024 spp 64 -> 256 +2.6 %, ecosys 64 spp
-    // 16 -> 64 +3.2 %, features2 512 spp 64 -> 128 even, 256 -1.7 %: too few units per wave;
-    // profiles/r03_loads/chunk.txt). Results do not depend on the chunking.
+    // Samples per work unit: a sixteenth of the launch (JT_CHUNKS_PER_LAUNCH). Under the per-lane
+    // work items a lane done with its pixel's chunk takes the next pixel at once, so short units
+    // cost no wave-level tail, and the launch ends on short units: measured against the round-3
+    // rule (LDS mode a quarter of the launch within [8, 64]; HBM mode >= 32 units per resident
+    // wave, up to 256 samples), cornellbox 256 spp +3.0 % (chunk 64 -> 16), its 1/2, 1/4, 1/8
+    // sample shares +3.7 %, +5 %, +5.4 % (128, 64, 32 spp: chunk 8, 4, 2), bathroom1 128 spp
+    // +1.3 %, features2 128 spp +0.4 %, ecosys 16 spp +5.7 % (gpurun_out/r04h/chunk,
+    // r04i/chunk). Results do not depend on the chunking.
     const int nsamp = s1 - s0;
     if (c->chunk > 0) {
         c->P.chunk = c->chunk;
-    } else if (c->lds_scene_bytes > 0) {
-        c->P.chunk = std::max(8, std::min(64, nsamp / 4));
     } else {
-        const long long waves = (long long)std::max(1, c->cus) * 16;  // 4 workgroups of 4 waves per CU
-        const long long tiles = (c->tiles + c->P.tile_stride - 1) / c->P.tile_stride;
-        const double target = std::max(8.0, (double)nsamp * (double)tiles / (double)(waves * 32));
-        // equal chunks: the nearest count of chunks per tile, at least enough for 256 samples each
-        const int nch = std::max({1, (int)std::lround(nsamp / target), (nsamp + 255) / 256});
-        c->P.chunk = std::max(1, (nsamp + nch - 1) / nch);
+        c->P.chunk = std::max(1, (nsamp + JT_CHUNKS_PER_LAUNCH - 1) / JT_CHUNKS_PER_LAUNCH);
     }
     // chunk table with a halving tail: full chunks while more than two remain, then halves down
     // to chunk_min samples, so the launch ends on short units (results do not depend on chunking)

@@ -17,10 +17,15 @@ actually binds, computed from PMC counters the same way for every workload:
   vmem_rd_gips    = SQ_INSTS_VMEM_RD / duration / 1e9        (vector-memory read wave-instructions/s)
   vmem_frac       = vmem_rd_gips / VMEM_PEAK_GIPS            (the measured dwordx4 gather ceiling,
                     profiles/r02_pair/td_width_bench.log mode 0: 2195 G lane-loads/s = 34.3 G/s)
+  vmem_mix_frac   = vmem_rd_gips / VMEM_MIX_PEAK_GIPS[traversal]   (the ceiling for the traversal's
+                    own node records, scripts/td_mix_bench.hip: 64-B wide records 40.6 G/s, 16-B
+                    binary node rows 34.7 G/s; profiles/r04_tdmix/)
+  td_unstalled_frac = td_busy_frac * (1 - TD_TC_STALL_sum / TD_TD_BUSY_sum)   (cycles the TD moves
+                    data rather than waits on the cache for it; agrees with vmem_mix_frac)
 
 The roof that binds (bench.py `roofline.bound`): "valu" for LDS-mode kernels (the scene is in LDS;
 issue of partly idle waves binds, frac = fp32_lane_frac), "vmem/TD" for HBM-mode kernels (node and
-primitive records are L2-resident and return through TD, frac = vmem_frac); hbm_frac beside it.
+primitive records are L2-resident and return through TD, frac = vmem_mix_frac); hbm_frac beside it.
 Every record carries `build`, the hash of the kernel sources and build flags it was measured on
 (`source_hash`); bench.py uses a record's counts only for the build it describes.
 
@@ -43,6 +48,16 @@ HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
 # an L2-resident array (scripts/td_width_bench.hip, profiles/r02_pair/td_width_bench.log mode 0:
 # 2195.0 G lane-loads/s / 64 lanes)
 VMEM_PEAK_GIPS = 2195.0 / 64
+# the same ceiling for the load each traversal order issues per node (scripts/td_mix_bench.hip,
+# profiles/r04_tdmix/rates.log, L2-resident working set, TD busy 0.93-0.99; a 2 GiB working set is
+# 1-25 % slower): the wide order's 64-B records are four dwordx4 of one record (40.60 G wave-instr/s),
+# the binary orders' 16-B node rows one dwordx4 (34.71)
+VMEM_MIX_PEAK_GIPS = {"wide": 40.60, "near": 34.71, "reference": 34.71}
+
+
+def record_traversal(rec):
+    m = re.search(r"traversal=(\w+)", rec.get("workload", ""))
+    return m.group(1) if m and m.group(1) in VMEM_MIX_PEAK_GIPS else "near"
 ROOT = __import__("pathlib").Path(__file__).resolve().parent.parent
 _HIPCC_VERSION = None
 
@@ -164,6 +179,9 @@ def derive(rec):
             out["vmem_rd_per_launch"] = pmc["SQ_INSTS_VMEM_RD"]
             out["vmem_rd_gips"] = pmc["SQ_INSTS_VMEM_RD"] / pd / 1e9
             out["vmem_frac"] = out["vmem_rd_gips"] / VMEM_PEAK_GIPS
+            out["vmem_mix_frac"] = out["vmem_rd_gips"] / VMEM_MIX_PEAK_GIPS[record_traversal(rec)]
+        if "td_busy_frac" in out and "td_tc_stall_frac_of_busy" in out:
+            out["td_unstalled_frac"] = out["td_busy_frac"] * (1.0 - out["td_tc_stall_frac_of_busy"])
     return {k: round(v, 6) for k, v in out.items()}
 
 
