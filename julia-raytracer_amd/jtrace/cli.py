@@ -3,8 +3,8 @@ ArgParse table (:12-86), the SAMPLER_TYPES index (:88) and Params (:90-138).
 
 Extensions beyond the reference (all optional): --seed (RNG seed), --width/--height (explicit
 image size, camera aspect := W/H), --device, --devices N (one context over GPUs 0..N-1:
-jt_create_multi), --missing (drop|error for incomplete scenes), --traversal (reference|near: BVH
-child visit order, include/jtrace.h jt_traversal).
+jt_create_multi), --missing (drop|error for incomplete scenes), --traversal (reference|near|wide|auto:
+the BVH traversal, include/jtrace.h jt_traversal).
 """
 from __future__ import annotations
 
