@@ -193,7 +193,7 @@ def main():
         state = trace.make_trace_state(sa, bvh, lights, jp, lib)
         abi.set_option(lib, "tile_share", None)
 
-    traversal = state.traversal  # "auto" resolved by the library: near from LDS, wide from HBM
+    traversal = state.traversal  # "auto" resolved by the library: wide for deep HBM-mode scenes, near otherwise
     img_t = None
     if world > 1:
         buf = state.device_buffers()

@@ -88,8 +88,9 @@ typedef enum jt_traversal {
     JT_TRAVERSAL_REFERENCE = 0,
     JT_TRAVERSAL_NEAR = 1,
     JT_TRAVERSAL_WIDE = 2,
-    JT_TRAVERSAL_AUTO = 3  /* near for a scene small enough to run from LDS, wide otherwise;
-                              jt_describe reports the order taken ("traversal=near|wide") */
+    JT_TRAVERSAL_AUTO = 3  /* wide for a scene that runs from HBM with a deep BVH (stack bound
+                              above 32), near otherwise (LDS-mode and shallow scenes); jt_describe
+                              reports the order taken ("traversal=near|wide") */
 } jt_traversal;
 
 /* CameraData (src/scene.jl:48-86), after the lookat conversion done by the loader. */

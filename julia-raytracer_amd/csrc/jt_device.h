@@ -14,6 +14,9 @@
 #ifndef JT_CHUNKS_PER_LAUNCH
 #define JT_CHUNKS_PER_LAUNCH 16  // the automatic chunk: a sixteenth of the launch's samples
 #endif
+#ifndef JT_AUTO_WIDE_MIN_STACK
+#define JT_AUTO_WIDE_MIN_STACK 32  // JT_TRAVERSAL_AUTO: wide records for HBM-mode scenes deeper than this
+#endif
 #ifndef JT_MAX_CHUNKS
 #define JT_MAX_CHUNKS 32
 #endif

@@ -708,7 +708,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     }
     // wide records (JT_TRAVERSAL_WIDE): the TLAS's, then every BLAS's; the binary node array is
     // then not uploaded. JT_TRAVERSAL_AUTO resolves to near for a small scene that runs from LDS
-    // and to wide otherwise (decided with the LDS blob below; the records are built then).
+    // or a shallow one, and to wide otherwise (decided with the LDS blob below; the records are
+    // built then).
     if (params->traversal < JT_TRAVERSAL_REFERENCE || params->traversal > JT_TRAVERSAL_AUTO)
         return bail(jt::fail(JT_ERR_INVALID, "traversal must be 0 (reference), 1 (near), 2 (wide) or 3 (auto)"));
     c->wide = params->traversal == JT_TRAVERSAL_WIDE;
@@ -984,7 +985,10 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         }
         c->lds_scene_bytes = S.blob_n16 ? bytes : 0;
     }
-    if (params->traversal == JT_TRAVERSAL_AUTO && !S.blob_n16) {
+    // auto: wide for a scene in HBM mode whose BVH is deep (a stack bound above 32: bathroom1 46,
+    // ecosys 43: +20 %, +30 % over near); near otherwise — features2 (bound 24) runs 2737/2742
+    // Mrays/s near vs 2677/2646 wide at 512 spp (gpurun_out/r04m), cornellbox runs from LDS
+    if (params->traversal == JT_TRAVERSAL_AUTO && !S.blob_n16 && need > JT_AUTO_WIDE_MIN_STACK) {
         // HBM mode: the wide records (the binary nodes stay uploaded, unused); the instances'
         // BLAS roots become root records
         if ((st = build_all_wide()) != JT_OK) return bail(st);

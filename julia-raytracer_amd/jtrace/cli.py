@@ -13,9 +13,9 @@ from dataclasses import dataclass
 
 SAMPLER_TYPES = ["path", "naive"]
 # BVH traversal of every product entry point (the CLI, Params, abi.make_params, bench.py and the
-# Julia shim): "auto" — the binary tree near child first ("near") for a scene that runs from LDS,
-# the 4-wide quantised records ("wide") otherwise, resolved by the library (jt_describe reports
-# which). "reference" is the reference's far-first order (src/bvh.jl:331-341); all differ only
+# Julia shim): "auto" — the 4-wide quantised records ("wide") for a scene that runs from HBM with
+# a deep BVH (stack bound above 32), the binary tree near child first ("near") otherwise, resolved
+# by the library (jt_describe reports which). "reference" is the reference's far-first order (src/bvh.jl:331-341); all differ only
 # where two hits tie at exactly equal t or a box is culled by the slab test's rounding.
 DEFAULT_TRAVERSAL = "auto"
 
@@ -59,7 +59,7 @@ def _parser() -> argparse.ArgumentParser:
     p.add_argument("--missing", choices=["error", "drop"], default="error",
                    help="missing scene assets: error (reference) or drop (extension)")
     p.add_argument("--traversal", choices=["reference", "near", "wide", "auto"], default=DEFAULT_TRAVERSAL,
-                   help="BVH traversal (extension): auto (default: near from LDS, wide otherwise), near "
+                   help="BVH traversal (extension): auto (default: wide for deep scenes in HBM, near otherwise), near "
                         "(binary, near child first), wide (4-wide quantised records) or reference (the "
                         "reference's far-first order); images differ only where two hits tie at exactly equal t")
     return p

@@ -158,7 +158,7 @@ class TraceState:
     @property
     def traversal(self) -> str:
         """The BVH traversal this context runs ("reference", "near" or "wide"): jt_params.traversal,
-        with "auto" resolved by the library (near when the scene runs from LDS, wide otherwise)."""
+        with "auto" resolved by the library (wide for a scene in HBM mode with a stack bound above 32, near otherwise)."""
         for tok in self.describe().split():
             if tok.startswith("traversal="):
                 return tok.split("=", 1)[1]

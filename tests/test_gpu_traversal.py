@@ -84,11 +84,12 @@ def test_near_order_rejects_bad_value(gpu, abi, lib, cornell_abi):
     assert e.value.status == -1
 
 
-@pytest.mark.parametrize("name,expect", [("cornellbox", "near"), ("bathroom1", "wide")])
+@pytest.mark.parametrize("name,expect", [("cornellbox", "near"), ("features2", "near"), ("bathroom1", "wide")])
 def test_auto_traversal_resolves_by_scene_mode(gpu, abi, lib, oracle, cornell_abi, name, expect):
-    """JT_TRAVERSAL_AUTO: near for a scene that runs from LDS (cornellbox), wide for one in HBM
-    mode (bathroom1); the render equals the explicit order's bit for bit and meets the parity bar
-    against the oracle's restatement of that order."""
+    """JT_TRAVERSAL_AUTO: near for a scene that runs from LDS (cornellbox) or a shallow one in HBM
+    mode (features2, stack bound 24), wide for a deep one (bathroom1, 46); the render equals the
+    explicit order's bit for bit and meets the parity bar against the oracle's restatement of
+    that order."""
     from jtrace import trace
     sa = cornell_abi if name == "cornellbox" else scene_abi(name)
     bvh = trace.make_scene_bvh(sa, False, lib)
