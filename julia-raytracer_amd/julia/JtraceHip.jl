@@ -180,10 +180,12 @@ end
 # Params src/cli.jl:90-138: camera is find_camera's 1-based index (src/jtrace.jl:61), sampler is
 # already the 1-based index into SAMPLER_TYPES = ["path", "naive"] (src/cli.jl:88,111-116) —
 # the C side's jt_sampler uses the same numbering — and clamp is an Int (src/cli.jl:105)
-# traversal (jt_traversal): 3 = auto, the product default (the binary tree near child first for a
-# scene that runs from LDS, the 4-wide quantised records otherwise), 1 = near, 2 = wide, 0 = the
+# traversal (jt_traversal): 3 = auto, the product default (the 4-wide quantised records for a deep
+# scene that runs from HBM, the binary tree near child first otherwise), 1 = near, 2 = wide, 0 = the
 # reference's far-first order (src/bvh.jl:331-341); they differ only where two hits tie at exactly
-# equal t or a box is culled by the slab test's rounding
+# equal t or a box is culled by the slab test's rounding (a few pixels per million per sample;
+# the share grows with spp: bench.py's reference-order line reports it at the configs' own spp).
+# JTRACE_TRAVERSAL=0 makes the drop-in trace_samples run the reference's exact order.
 pack_params(p::Params; device = 0, seed = 0x5EED, traversal = 3) =
     JtParams(Int32(p.camera - 1), Int32(p.resolution), Int32(0), Int32(0), Int32(p.samples), Int32(p.bounces),
              Int32(p.sampler), Int32(p.clamp), Int32(p.envhidden), Int32(p.tentfilter), Int32(p.nocaustics),
@@ -202,10 +204,10 @@ jt_create_multi over GPUs 0 .. devices-1 — every trace_samples batch is sharde
 samples, or by pixel tiles when a batch has fewer samples than devices) and get_image! returns
 their RCCL-reduced running mean."""
 function make_hip_state(scene::SceneData, bvh::SceneBvh, lights::TraceLights, params::Params; device = 0,
-                        devices = 1)
+                        devices = 1, traversal = 3)
     keep = Any[]
     cs = Ref(pack_scene(scene, keep)); cb = Ref(pack_bvh(bvh, keep)); cl = Ref(pack_lights(lights, keep))
-    cp = Ref(pack_params(params; device = device))
+    cp = Ref(pack_params(params; device = device, traversal = traversal))
     ctx = Ref{Ptr{Cvoid}}(C_NULL)
     GC.@preserve keep cs cb cl cp begin
         if devices > 1
@@ -263,7 +265,8 @@ function trace_samples(state::TraceState, scene::SceneData, bvh::SceneBvh, light
         return
     end
     hip = get!(CONTEXTS, state) do
-        make_hip_state(scene, bvh, lights, params; devices = parse(Int, get(ENV, "JTRACE_DEVICES", "1")))
+        make_hip_state(scene, bvh, lights, params; devices = parse(Int, get(ENV, "JTRACE_DEVICES", "1")),
+                       traversal = parse(Int, get(ENV, "JTRACE_TRAVERSAL", "3")))
     end
     trace_samples(hip, state)
 end
