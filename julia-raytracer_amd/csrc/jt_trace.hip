@@ -1076,12 +1076,12 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     const int smp = c->sampler == JT_SAMPLER_NAIVE ? 2 : 1;
     const bool lstep = inst_light && smp == 1 && (light_steps(smp, c->kmask) || c->S.light_inline);
     // deep BVHs (stack bound > 32: bathroom1, ecosys) shade sooner: their lanes finish queries far
-    // apart, so waiting for many leaves the wave idle. Measured with inline light chains
-    // (profiles/r03_inline/wl.txt, ab_fp_nr.txt): cornellbox 56, features2 60 (56: -1.5 %, 64:
-    // -1 %), bathroom1 40 (32: -0.8 %, 48: -1.4 %); without instance lights (ecosys) 16 (40 -> 16
-    // was +15 %)
+    // apart, so waiting for many leaves the wave idle. Re-swept in round 4 (per-lane work items,
+    // short chunks, auto traversal; profiles/r04_ab/wait_lanes_r04o.txt): cornellbox 56 (52
+    // even, 48 / 60 -1.3 %, 64 -6 %), features2 56 (60 -2.9 %, 48 -0.5 %, 64 -9 %), bathroom1 40
+    // (48 even, 24 -10 %), ecosys (no instance lights) 24 (16 -1.2 %, 32 -2.2 %, 8 -11 %)
     const bool deep = c->stack > 32;
-    P.wait_lanes = lstep ? (deep ? 40 : ft_none(c->kmask) ? 56 : 60) : deep ? 16 : 40;
+    P.wait_lanes = lstep ? (deep ? 40 : 56) : deep ? 24 : 40;
     if (const char* wl = opt("wait_lanes")) P.wait_lanes = std::max(1, std::min(64, std::atoi(wl)));
     P.light_lanes = 2;
     if (const char* ll = opt("light_lanes")) P.light_lanes = std::max(1, std::min(65, std::atoi(ll)));
