@@ -179,7 +179,7 @@ def main():
             "lights_s": round(t_lights - t_bvh, 3), "upload_s": round(t_create - t_lights, 3),
             "total_s": round(t_create - t_0, 3)}
     W, H, S = state.width, state.height, args.spp
-    from jtrace.parallel import (compare_signature, image_signature, load_signature,
+    from jtrace.parallel import (PipelinedReduce, compare_signature, image_signature, load_signature,
                                  save_signature, split_plan)
     # this rank's share: 1/G of the 8x8 tiles (G = --tile-groups) x a contiguous
     # 1/(N/G) of the samples; G = 1 is the pure sample split
@@ -205,37 +205,28 @@ def main():
 
     reduced = [None]  # rank 0, N > 1: the last step's reduced image (the image check below)
     # N > 1: the path's one exchange, the sum of sample-weighted shard means onto rank 0 (RCCL),
-    # pipelined: a step snapshots its weighted shard image into one of two buffers and starts the
-    # reduce asynchronously, so it runs during the next step's launch; a buffer is reused only
-    # after its previous reduce completed, and drain() ends the last one inside the timed region
-    snaps, pending, last = [], [None, None], [0]
+    # pipelined (jtrace.parallel.PipelinedReduce): a step snapshots its weighted shard image into
+    # one of two buffers and starts the reduce asynchronously, so it runs during the next step's
+    # launch; the snapshot reads the library's buffer on torch's stream, so it is finished before
+    # the next step's jt_reset clears that buffer on the library's stream; drain() ends the last
+    # reduce inside the timed region
+    red = None
     if world > 1:
-        snaps = [torch.empty(H * W * 4, dtype=torch.float32, device=img_t.device if backend == "nccl" else "cpu")
-                 for _ in range(2)]
+        red = PipelinedReduce(H * W * 4, s1 - s0, S, dist, device=img_t.device if backend == "nccl" else "cpu",
+                              sync=torch.cuda.current_stream().synchronize)
 
     def step():
         state.reset()
         state.trace_range(s0, s1)  # returns when the launch has finished (HIP event sync)
-        if world > 1:
-            i = (last[0] + 1) % 2
-            if pending[i] is not None:
-                pending[i].wait()
-            torch.mul(img_t if backend == "nccl" else img_t.cpu(), float(s1 - s0), out=snaps[i])
-            # the snapshot reads the library's buffer on torch's stream: finish it before the next
-            # step's jt_reset clears that buffer on the library's stream
-            torch.cuda.current_stream().synchronize()
-            pending[i] = dist.reduce(snaps[i], dst=0, op=dist.ReduceOp.SUM, async_op=True)
-            last[0] = i
+        if red is not None:
+            red.submit(img_t if backend == "nccl" else img_t.cpu())
         return state.counters()
 
     def drain():
-        for i in range(len(pending)):
-            if pending[i] is not None:
-                pending[i].wait()
-                pending[i] = None
+        out = red.drain() if red is not None else None
         torch.cuda.synchronize()
-        if world > 1 and rank == 0:
-            reduced[0] = snaps[last[0]] / float(S)
+        if out is not None:
+            reduced[0] = out
 
     for _ in range(args.warmup):
         step()

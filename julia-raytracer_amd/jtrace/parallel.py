@@ -45,6 +45,44 @@ def reduce_running_means(tensor, n_local: int, n_total: int, dist, dst: int = 0)
     return part
 
 
+class PipelinedReduce:
+    """The bench's per-step reduce of sample-weighted shard means onto `dst`, pipelined: submit()
+    snapshots the shard image (times n_local) into one of two buffers and starts the reduce
+    asynchronously, so it runs during the next step's launch; a buffer is reused only after its
+    previous reduce completed. `sync` (the GPU: the current stream's synchronize) returns once
+    the snapshot is taken, so the caller may overwrite `src` (the library's next jt_reset).
+    drain() completes every reduce and returns the last submitted step's combined mean on `dst`
+    (None elsewhere)."""
+
+    def __init__(self, numel: int, n_local: int, n_total: int, dist, device="cpu", dst: int = 0, sync=None):
+        import torch
+        self.torch, self.dist, self.dst, self.sync = torch, dist, dst, sync
+        self.n_local, self.n_total = float(n_local), float(n_total)
+        self.bufs = [torch.empty(numel, dtype=torch.float32, device=device) for _ in range(2)]
+        self.pending = [None, None]
+        self.last = None
+
+    def submit(self, src):
+        i = 0 if self.last is None else 1 - self.last
+        if self.pending[i] is not None:
+            self.pending[i].wait()
+            self.pending[i] = None
+        self.torch.mul(src, self.n_local, out=self.bufs[i])
+        if self.sync is not None:
+            self.sync()
+        self.pending[i] = self.dist.reduce(self.bufs[i], dst=self.dst, op=self.dist.ReduceOp.SUM, async_op=True)
+        self.last = i
+
+    def drain(self):
+        for i in range(2):
+            if self.pending[i] is not None:
+                self.pending[i].wait()
+                self.pending[i] = None
+        if self.last is None or self.dist.get_rank() != self.dst:
+            return None
+        return self.bufs[self.last] / self.n_total
+
+
 def all_reduce_running_means(tensor, n_local: int, n_total: int, dist):
     part = tensor * float(n_local)
     dist.all_reduce(part, op=dist.ReduceOp.SUM)

@@ -1,6 +1,7 @@
 """N > 1 path on the CPU: world_size-2 gloo. Each rank renders its sample shard (the oracle
 stands in for the GPU kernel, which is bit-identical to it) and the shards are combined with
-the same reduce the bench runs over RCCL (jtrace.parallel.reduce_running_means)."""
+the same reduce the bench runs over RCCL (jtrace.parallel.reduce_running_means, and its pipelined
+form jtrace.parallel.PipelinedReduce)."""
 import os
 import sys
 
@@ -30,8 +31,19 @@ def _worker(rank, world, port, out_path):
     s0, s1 = shard_range(SPP, world, rank)
     img = orc.trace(sa, orc.build_bvh(sa), orc.make_lights(sa), p, RES, RES, s0, s1, first=s0, nthreads=2)[0]
     out = reduce_running_means(torch.from_numpy(img), s1 - s0, SPP, dist, dst=0)
+    # the bench's pipelined form: three steps through two buffers, the last one the real image
+    # (earlier steps' reduces must not leak into it, and a buffer is reused only once reduced)
+    from jtrace.parallel import PipelinedReduce
+    red = PipelinedReduce(img.size, s1 - s0, SPP, dist)
+    src = torch.empty(img.size, dtype=torch.float32)
+    for scale in (3.0, 7.0, 1.0):
+        src.copy_(torch.from_numpy(img).reshape(-1) * scale)
+        red.submit(src)
+        src.fill_(-1.0)  # the caller overwrites its buffer after submit (the next jt_reset)
+    piped = red.drain()
     if rank == 0:
         np.save(out_path, out.numpy())
+        np.save(str(out_path) + ".piped.npy", piped.reshape(out.shape).numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -44,6 +56,7 @@ def test_two_rank_shards_equal_single_render(abi, oracle, cornell_abi, tmp_path)
     out = tmp_path / "img.npy"
     mp.spawn(_worker, args=(2, port, str(out)), nprocs=2, join=True)
     combined = np.load(out)
+    np.testing.assert_array_equal(np.load(str(out) + ".piped.npy"), combined)
     p = make_params(abi, resolution=RES, samples=SPP)
     single = oracle.trace(cornell_abi, oracle.build_bvh(cornell_abi), oracle.make_lights(cornell_abi), p, RES, RES,
                           0, SPP)[0]
