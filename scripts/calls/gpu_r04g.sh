@@ -12,4 +12,4 @@ scripts/gpu_step.sh 400 $O/bench.log python bench.py || exit 1
 AB_SCENES="cb" bash scripts/gpu_lib_ab.sh $1/ab_cb base nonxt || exit 1
 AB_SCENES="f2 b1" AB_ARGS="--traversal near" bash scripts/gpu_lib_ab.sh $1/ab_near base nonxt || exit 1
 AB_F2_SPP=128 AB_B1_SPP=128 AB_EC_SPP=16 bash scripts/gpu_lib_ab.sh $1/ab_parkw base parkw parkw3 || exit 1
-bash scripts/gpu_r04f.sh $1/shares || exit 1
+bash scripts/calls/gpu_r04f.sh $1/shares || exit 1
