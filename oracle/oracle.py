@@ -91,6 +91,9 @@ class Oracle:
     def trace(self, scene_abi, bvh, lights, params, width, height, s0, s1, first=0, rows=None,
               nthreads=None, state=None):
         """Returns (image (H,W,4), albedo (H,W,3), normal (H,W,3), hits (H,W), counters)."""
+        if params.traversal not in (0, 1, 2):
+            raise ValueError(f"the oracle restates an explicit BVH order (0 reference, 1 near, 2 wide), got "
+                             f"{params.traversal}: resolve auto (3) to the order the library ran first")
         if nthreads is None:
             nthreads = min(16, os.cpu_count() or 1)
         if state is None:

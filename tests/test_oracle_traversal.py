@@ -76,3 +76,11 @@ def test_wide_records_are_conservative(abi, oracle, name):
     assert c["violations"] == 0
     assert c["leaves"] == leaves
     assert 1.0 <= c["volume_ratio"] < 2.0
+
+
+def test_oracle_rejects_unresolved_auto(abi, oracle, cornell_abi):
+    """The oracle restates an explicit order: "auto" (3) is the library's choice by scene mode and
+    depth, so a checker must pass the order the library resolved (bench.py's CPU leg, smoke())."""
+    p = make_params(abi, resolution=8, samples=1, traversal="auto")
+    with pytest.raises(ValueError):
+        oracle.trace(cornell_abi, oracle.build_bvh(cornell_abi), oracle.make_lights(cornell_abi), p, 8, 8, 0, 1)
