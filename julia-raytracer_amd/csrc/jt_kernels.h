@@ -396,23 +396,13 @@ __device__ __forceinline__ bool query_busy(const Trav& T) { return T.sp > 0 || T
 // A lane's next step in either traversal: a primitive test (nprim > 0) or a node step (a stack
 // entry, or in the wide traversal a pending child word); neither: its query is done (sp 0) or the
 // lane has no samples left (sp < 0).
-// JT_BIN_NXT: the binary traversal keeps the entry it pops next in a register (Trav::nxt) instead
-// of pushing it and popping it back: an internal node pushes only its second child, a TLAS leaf all
-// but its first instance. The same entries in the same order (results and counters unchanged; the
-// GPU suite passed on it), one LDS write and one dependent LDS read fewer per internal node — but
-// measured slower where the binary order runs in production: cornellbox 9922/9907 vs 10027/9981
-// Mrays/s without it (-0.9 %); near order in HBM mode features2 and bathroom1 within +-1 %
-// (gpurun_out/r04g/ab_cb, ab_near). Off.
-#ifndef JT_BIN_NXT
-#define JT_BIN_NXT 0
-#endif
 template <bool WIDE>
 __device__ __forceinline__ bool wants_node(const Trav& T) {
-    return T.nprim == 0 && (T.sp > 0 || ((WIDE || JT_BIN_NXT) && T.nxt != W_EMPTY));
+    return T.nprim == 0 && (T.sp > 0 || (WIDE && T.nxt != W_EMPTY));
 }
 template <bool WIDE>
 __device__ __forceinline__ bool query_done(const Trav& T) {
-    return (T.sp | T.nprim) == 0 && (!(WIDE || JT_BIN_NXT) || T.nxt == W_EMPTY);
+    return (T.sp | T.nprim) == 0 && (!WIDE || T.nxt == W_EMPTY);
 }
 
 __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d, unsigned root, int* stack) {
@@ -434,15 +424,10 @@ __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d
     T.cur_kind = KIND_TRI;
     T.inst_space = 0;
     T.negmask = neg_mask(d, S.order_flip);
+    stack[0] = (int)root;
+    T.sp = 1;
     T.low = 0;
-    if (JT_BIN_NXT) {
-        T.sp = 0;
-        T.nxt = root;
-    } else {
-        stack[0] = (int)root;
-        T.sp = 1;
-        T.nxt = W_EMPTY;
-    }
+    T.nxt = W_EMPTY;
 }
 // query_begin of the wide traversal: the root is the first node step's child word (the TLAS
 // root record, or an instance leaf of one instance for intersect_instance_bvh); the stack is empty
@@ -581,16 +566,7 @@ template <int RING, bool OVF, int COUNT, bool NCACHE, int F>
 __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
     // without FT_XFORM every instance ray is the world ray: no transform, no space switch
     constexpr bool XF = (F & FT_XFORM) != 0;
-    unsigned e;
-    if (JT_BIN_NXT) {  // the pending entry, else the stack's top
-        const bool held = T.nxt != W_EMPTY;
-        unsigned p = 0;
-        if (!held) p = st_pop<RING, OVF>(S, T, stack, pixel);
-        e = held ? T.nxt : p;
-        T.nxt = W_EMPTY;
-    } else {
-        e = st_pop<RING, OVF>(S, T, stack, pixel);
-    }
+    const unsigned e = st_pop<RING, OVF>(S, T, stack, pixel);
     unsigned type = e >> 30, idx = e & IDX_MASK;
     if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
         if (COUNT) cnt.instances++;
@@ -663,22 +639,15 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             const bool k1 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n1.a, n1.b);
             if (COUNT) cnt.nodes += (k0 ? 0 : 1) + (k1 ? 0 : 1);
             const unsigned ptag = type << 30 | (unsigned)T.nh << 24;  // pre-tested at hit count nh
-            if (JT_BIN_NXT) {  // the child popped next stays in nxt
-                if (k0 && k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_second);
-                if (k0 || k1) T.nxt = ptag | (k1 ? c_first : c_second);
-            } else {
-                if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_second);
-                if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_first);
-            }
+            if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_second);
+            if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_first);
         } else {
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_second);
-            if (JT_BIN_NXT) T.nxt = tag | c_first;
-            else st_push<RING, OVF>(S, T, stack, pixel, tag | c_first);
+            st_push<RING, OVF>(S, T, stack, pixel, tag | c_first);
         }
     } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
-        for (int k = num - 1; k >= (JT_BIN_NXT ? 1 : 0); k--)
+        for (int k = num - 1; k >= 0; k--)
             st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | SNAP_NONE | (unsigned)(start + k));
-        if (JT_BIN_NXT && num > 0) T.nxt = (T_INST << 30) | SNAP_NONE | (unsigned)start;
     } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
@@ -710,18 +679,6 @@ __device__ __forceinline__ void wide_box(const float4& r0, const uint4& r1, cons
     const int sh = 8 * c;
     a = make_float4(deq(r0.x, r1.x, sh, sx), deq(r0.x, r1.y, sh, sx), deq(r0.y, r1.z, sh, sy), deq(r0.y, r1.w, sh, sy));
     b = make_float4(deq(r0.z, r2.x, sh, sz), deq(r0.z, r2.y, sh, sz), 0.0f, 0.0f);
-}
-// packed slab pairs in the wide visit: measured slower (bathroom1 -3 %, ecosys -2 %; gpurun_out/r04d/abpk)
-#ifndef JT_WIDE_PK
-#define JT_WIDE_PK 0
-#endif
-typedef float f2v __attribute__((ext_vector_type(2)));
-// (lo - o) * dinv, (hi - o) * dinv of one axis of a dequantised box: lo / hi = origin + byte * scale
-// (exact product, one rounding: fma), then the reference's slab products (src/geometry.jl:96-105)
-__device__ __forceinline__ f2v slab_pair(unsigned wlo, unsigned whi, int sh, float s, float origin, float o, float dinv) {
-    const f2v q = {(float)((wlo >> sh) & 255u), (float)((whi >> sh) & 255u)};
-    const f2v b = __builtin_elementwise_fma(q, (f2v){s, s}, (f2v){origin, origin});
-    return (b - (f2v){o, o}) * (f2v){dinv, dinv};
 }
 // intersect_bbox's decision from the six slab values (mx, Mx, my, My, mz, Mz), as intersect_bbox
 __device__ __forceinline__ bool slab_test(float mx, float Mx, float my, float My, float mz, float Mz, float tmin, float tmax) {
@@ -759,19 +716,9 @@ __device__ __forceinline__ void wide_visit(const DScene& S, Trav& T, int* stack,
     unsigned hits = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-#if JT_WIDE_PK
-        // the reference's slab test on the dequantised box, each axis's two planes as one packed
-        // pair (v_pk_fma / v_pk_add / v_pk_mul: the same IEEE operations, half the instructions)
-        const int sh = 8 * c;
-        const f2v tx = slab_pair(r1.x, r1.y, sh, sx, r0.x, T.lo.x, T.ldinv.x);
-        const f2v ty = slab_pair(r1.z, r1.w, sh, sy, r0.y, T.lo.y, T.ldinv.y);
-        const f2v tz = slab_pair(r2.x, r2.y, sh, sz, r0.z, T.lo.z, T.ldinv.z);
-        const bool pass = slab_test(tx.x, tx.y, ty.x, ty.y, tz.x, tz.y, ray_eps, T.tmax);
-#else
         float4 a, b;
         wide_box(r0, r1, r2, sx, sy, sz, c, a, b);
         const bool pass = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, a, b);
-#endif
         if (wide_word(r3, c) != W_EMPTY && pass) hits |= 1u << c;
     }
     if (!hits) return;
@@ -937,15 +884,7 @@ constexpr unsigned CTL_BOUNCE = 0x7fffu, CTL_OPB = 15, CTL_FLAGS = 23, CTL_LC = 
 #ifndef JT_PARK_PB
 #define JT_PARK_PB 1
 #endif
-// weight (the path throughput) is read and written only in the shading code as well; parked in
-// slots [8, 11) it frees three registers across the traversal loop (JT_PARK_W): features2's kernel
-// then spills nothing (3 VGPRs and 2 in-loop scratch stores per shade without it), but its 43 KiB
-// of LDS per workgroup fit only 3 workgroups per CU instead of 4: features2 -12 %, bathroom1 -14 %,
-// ecosys -13 %, and as much at 3 waves with 168 VGPRs (gpurun_out/r04g/ab_parkw). Off.
-#ifndef JT_PARK_W
-#define JT_PARK_W 0
-#endif
-constexpr int PARK_SLOTS = 7 + (JT_PARK_PB ? 1 : 0) + (JT_PARK_PB && JT_PARK_W ? 3 : 0);  // radiance xyz, max_roughness, lq xyz, pb, weight xyz
+constexpr int PARK_SLOTS = 7 + (JT_PARK_PB ? 1 : 0);  // radiance xyz, max_roughness, lq xyz, pb
 // slots: [0, 3) radiance, 3 max_roughness, [4, 7) lq, 7 pb. The mesh kernels park (features2 +6 %,
 // bathroom1 +14 %, ecosys +9 %: their spills fell from 12-28 to 0-7 VGPRs). The FT_NONE kernel
 // (cornellbox, 2-8 spilled VGPRs either way) does not: its light-hit steps read the light-chain
@@ -1003,20 +942,12 @@ struct Path {
         if (park(F) && JT_PARK_PB) pk[7 * BLOCK] = v;
         else pb_ = v;
     }
+    // the path weight stays in registers (parked in three more LDS slots it cost the texture
+    // kernels a workgroup per CU: DESIGN.md §2 Experiments)
     template <int F>
-    __device__ __forceinline__ v3 weight() const {
-        return park(F) && JT_PARK_PB && JT_PARK_W ? V3(pk[8 * BLOCK], pk[9 * BLOCK], pk[10 * BLOCK]) : weight_;
-    }
+    __device__ __forceinline__ v3 weight() const { return weight_; }
     template <int F>
-    __device__ __forceinline__ void set_weight(v3 v) {
-        if (park(F) && JT_PARK_PB && JT_PARK_W) {
-            pk[8 * BLOCK] = v.x;
-            pk[9 * BLOCK] = v.y;
-            pk[10 * BLOCK] = v.z;
-        } else {
-            weight_ = v;
-        }
-    }
+    __device__ __forceinline__ void set_weight(v3 v) { weight_ = v; }
     __device__ __forceinline__ int bounce() const { return (int)(ctl & CTL_BOUNCE); }
     __device__ __forceinline__ int opbounce() const { return (int)((ctl >> CTL_OPB) & 0xffu); }
     __device__ __forceinline__ bool flag(int f) const { return (ctl >> CTL_FLAGS) & (unsigned)f; }
@@ -1851,9 +1782,18 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
 #ifndef JT_LANE_ITEMS
 #define JT_LANE_ITEMS 1
 #endif
+// JT_ITEM_FIRST_POP: a sample's first node pops run at its start, in the hand-out, where most of
+// the wave's lanes start samples together (1: every kernel, 0: none, 2: the binary-order mesh
+// kernels only). Measured in round 4 (profiles/r04_ab/knobs*_r04[rs].txt, two runs each), off
+// against on: cornellbox +0.4 % (10317/10318 vs 10273/10277 Mrays/s), bathroom1 and ecosys (wide)
+// +1.2 % and even, features2 (near, mesh) -1.5 % (2666/2679 vs 2722/2709). 2.
 #ifndef JT_ITEM_FIRST_POP
-#define JT_ITEM_FIRST_POP 1
+#define JT_ITEM_FIRST_POP 2
 #endif
+template <bool WIDE, int F>
+__host__ __device__ constexpr bool item_first_pop() {
+    return JT_ITEM_FIRST_POP == 1 || (JT_ITEM_FIRST_POP == 2 && !WIDE && !ft_none(F));
+}
 // a lane's item: bits 0-25 the pixel's slot tile * 64 + l (l: pixel of the 8x8 tile; jt_create
 // keeps tiles below 2^20), 26-30 its chunk, 31 ITEM_BLOCKED (taken, waiting for the previous
 // chunk of the pixel); ITEM_NONE: no pixel
@@ -1990,11 +1930,11 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
             start_path<F>(P, pixel % P.width, pixel / P.width, pixel, sample, st);
             query_start<WIDE>(S, T, st.o, st.d, -1, stack);
             if (!WC) lds_count(1, true);
-#if JT_ITEM_FIRST_POP
+            if constexpr (item_first_pop<WIDE, F>()) {
 #pragma unroll
-            for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
-                if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
-#endif
+                for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
+                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
+            }
         }
         if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(start));
         if (__builtin_amdgcn_ballot_w64(item != ITEM_NONE) == 0) break;  // drained, and every lane is done
