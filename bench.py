@@ -115,8 +115,9 @@ def main():
     ap.add_argument("--sampler", default="path")
     ap.add_argument("--scene", default=str(ROOT / "assets" / "scenes" / "cornellbox" / "cornellbox.json"))
     ap.add_argument("--traversal", choices=["reference", "near", "wide", "auto"], default=DEFAULT_TRAVERSAL,
-                    help="BVH child order (include/jtrace.h jt_traversal): near child first (the default, the "
-                         "product's order) or the reference's far-first order (src/bvh.jl:331-341)")
+                    help="BVH child order (include/jtrace.h jt_traversal): auto (the default: wide records for "
+                         "deep HBM-mode scenes, near child first otherwise), near, wide, or the reference's "
+                         "far-first order (src/bvh.jl:331-341)")
     ap.add_argument("--no-reference-order", action="store_true",
                     help="skip the reference-order comparison line (rank 0, N=1, --traversal near)")
     ap.add_argument("--highqualitybvh", action="store_true",
@@ -125,11 +126,14 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-spp", type=int, default=128)
     ap.add_argument("--tile-groups", type=int, default=0,
-                    help="N > 1: split the tiles into G interleaved groups x N/G sample ranges (0: automatic)")
+                    help="N > 1: split the tiles into G interleaved groups x N/G sample ranges (0 or 1: the pure "
+                         "sample split)")
     ap.add_argument("--as-rank-of", type=int, default=0,
                     help="N=1: trace rank 0's share of an N-rank run (per-GPU rate and roofline of that share)")
     ap.add_argument("--write-signature", action="store_true",
                     help="N=1: record this workload's image fingerprint in profiles/image_signatures.json")
+    ap.add_argument("--print-workload", action="store_true",
+                    help="print the workload key of this run's roofline record (scripts/gpu_measure.sh) and exit")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="a library run-time option (jt_set_option, include/jtrace.h) for A/B runs; repeatable")
     args = ap.parse_args()
@@ -194,6 +198,14 @@ def main():
         abi.set_option(lib, "tile_share", None)
 
     traversal = state.traversal  # "auto" resolved by the library: wide for deep HBM-mode scenes, near otherwise
+    workload = f"{Path(args.scene).stem} {args.sampler} {W}x{H} {s1 - s0} samples/launch" + \
+        (f" tiles 1/{groups}" if groups > 1 else "") + \
+        ("" if traversal == "reference" else f" traversal={traversal}") + \
+        (" bvh=sah" if args.highqualitybvh else "")
+    if args.print_workload:
+        print(workload, flush=True)
+        state.close()
+        return
     img_t = None
     if world > 1:
         buf = state.device_buffers()
@@ -355,10 +367,6 @@ def main():
         per_launch = {k: v / max(1, full["launches"]) for k, v in full.items()}  # one step's launches
         logical = algorithmic_bytes(per_launch, shade_record_bytes(scene),
                                     any(len(s.quads) for s in scene.shapes), traversal == "wide")
-        workload = f"{name} {args.sampler} {W}x{H} {s1 - s0} samples/launch" + \
-            (f" tiles 1/{groups}" if groups > 1 else "") + \
-            ("" if traversal == "reference" else f" traversal={traversal}") + \
-            (" bvh=sah" if args.highqualitybvh else "")
         sys.path.insert(0, str(ROOT / "scripts"))
         from roofline import VMEM_MIX_PEAK_GIPS
         # the source hash the Makefile embedded in the library that ran (jt_version), not a hash of

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define JT_ABI_VERSION 3  /* 2: jt_params.traversal; 3: jt_set_option */
+#define JT_ABI_VERSION 4  /* 2: jt_params.traversal; 3: jt_set_option; 4: sample streams, jt_get_streams */
 
 typedef enum jt_status {
     JT_OK = 0,
@@ -275,10 +275,12 @@ int jt_device_count(int32_t* out);
  *   "lds_scene" "<bytes>"    budget of the small-scene LDS blob (0: scene arrays stay in HBM)
  *   "lds_stack" "32"         a 32-entry LDS stack ring instead of 16
  *   "light_inline" "0"       sample_lights_pdf's light queries through the traversal loop
- *   "chunk", "chunk_min"     samples per work unit; the halving tail of the chunk table
  *   "wait_lanes", "light_lanes"  the shading gate; the light-hit step gate
  *   "multi_split" "tiles"|"samples"  jt_create_multi's split mode
  * Options that change WHAT a context traces (jt_describe reports them when set):
+ *   "streams" "<k>"          sample streams per pixel (a power of two <= 64) instead of the
+ *                            automatic count (jt_get_streams): the running means combine in a
+ *                            different order, so images differ in the last bits
  *   "tile_share" "k,o"       trace only the 8x8 tiles o, o + k, o + 2k, ...: this process's share
  *                            of a k-way tile split when one process per GPU shards a render by
  *                            tiles (bench.py); jt_create_multi sets its own split instead
@@ -326,9 +328,20 @@ int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lig
 /* trace_samples (src/trace.jl:215-274): samples [n, min(n+batch, samples)), n += batch. */
 int jt_trace_samples(jt_ctx* ctx);
 /* Accumulate global samples [sample_begin, sample_end) into the running mean, in order.
- * The running-mean weight of global sample s is 1/(s - first_sample + 1) where
- * first_sample is the first sample this context ever traced (0 for a single device). */
+ * Sample streams (fixed per context, jt_get_streams: k, a power of two): local sample
+ * t = s - first_sample (first_sample: the first sample this context ever traced, 0 for a single
+ * device) belongs to stream j = t mod k and is the c-th sample of that stream, c = t div k; every
+ * stream keeps its own running mean (src/trace.jl:631-648, weight 1/(c + 1)), and after every
+ * call the image / AOVs are the streams' means combined in stream order,
+ *     image = sum_{j < min(k, n)} mean_j * w_j,  w_j = (float)((double)n_j / n),
+ * n the local samples so far and n_j those of stream j (float multiply-adds without FMA,
+ * starting from mean_0 * w_0); hits = sum_j hits_j. k = 1 is the reference's single running mean.
+ * The result does not depend on how a render is split into calls. */
 int jt_trace_range(jt_ctx* ctx, int32_t sample_begin, int32_t sample_end);
+/* The context's sample streams per pixel k (jt_trace_range). Chosen by jt_create: 1 when
+ * params->batch is 1 (the reference's default); otherwise the largest power of two k <= 64,
+ * k <= batch, with (pixels the context traces) * k <= 2^24 (at least 1), or the "streams" option. */
+int jt_get_streams(const jt_ctx* ctx, int32_t* streams);
 int jt_get_samples(const jt_ctx* ctx, int32_t* samples);
 int jt_get_size(const jt_ctx* ctx, int32_t* width, int32_t* height);
 int jt_get_image(jt_ctx* ctx, float* rgba);                          /* W*H*4 */

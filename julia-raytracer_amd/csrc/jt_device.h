@@ -11,14 +11,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#ifndef JT_CHUNKS_PER_LAUNCH
-#define JT_CHUNKS_PER_LAUNCH 16  // the automatic chunk: a sixteenth of the launch's samples
+#ifndef JT_STREAM_ITEMS
+#define JT_STREAM_ITEMS (1 << 24)  // automatic stream count: about this many (pixel, stream) items
 #endif
 #ifndef JT_AUTO_WIDE_MIN_STACK
 #define JT_AUTO_WIDE_MIN_STACK 32  // JT_TRAVERSAL_AUTO: wide records for HBM-mode scenes deeper than this
 #endif
-#ifndef JT_MAX_CHUNKS
-#define JT_MAX_CHUNKS 32
+#ifndef JT_MAX_STREAMS
+#define JT_MAX_STREAMS 64  // sample streams per pixel (a power of two, jt_ctx::streams)
 #endif
 #ifndef JT_EXACT_MATH
 #define JT_EXACT_MATH 1
@@ -204,15 +204,14 @@ struct DParams {
     int bounces, sampler;
     float clamp;
     int envhidden, tentfilter, nocaustics;
-    int first;  // running-mean origin: weight of sample s is 1/(s - first + 1)
+    int first;  // running-mean origin: local sample t = s - first
+    // sample streams (DESIGN.md §2 "Sample streams"): local sample t belongs to stream
+    // t & (2^lk - 1) and is the (t >> lk)-th sample of that stream's own running mean, weight
+    // 1/((t >> lk) + 1); the launch ends by combining the streams' means (jt_trace.hip combine)
+    int lk;
     int wait_lanes;
     int light_lanes;  // path sampler: run a light-hit step inside the traversal phase once this
                       // many lanes wait on a sample_lights_pdf query result (65: never)
-    int chunk;  // samples per work unit (a tile's chunks run in order)
-    // chunk table (nct > 0): chunk c covers samples [s_begin + cbeg[c], s_begin + cbeg[c+1]) —
-    // full chunks, then a halving tail that shortens the launch's last units (JT_CHUNK_MIN)
-    int nct;
-    int cbeg[JT_MAX_CHUNKS + 1];
     // the 8x8 tiles this launch covers: t = k * tile_stride + tile_offset (a multi-device context
     // split by pixel tiles, jt_create_multi; 1 / 0 otherwise: every tile)
     int tile_stride, tile_offset;

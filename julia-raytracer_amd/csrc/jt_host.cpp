@@ -28,8 +28,8 @@ int fail(int status, const std::string& msg) {
 static std::mutex g_opt_mu;
 static std::map<std::string, std::string> g_opts;
 static const char* const kOptionNames[] = {
-    "env_alias",  "features",    "lds_scene",   "lds_stack",  "light_inline", "chunk",
-    "chunk_min",  "wait_lanes",  "light_lanes", "multi_split", "tile_share",  "test_lds_ring",
+    "env_alias",  "features",    "lds_scene",   "lds_stack",  "light_inline", "streams",
+    "wait_lanes", "light_lanes", "multi_split", "tile_share",  "test_lds_ring",
 };
 std::map<std::string, std::string> options_snapshot() {
     std::lock_guard<std::mutex> g(g_opt_mu);

@@ -1101,10 +1101,12 @@ struct Aov {
     float* acc;
     float w_;    // !lane_lds(F)
     int first_;  // params.first (the weight's sample offset)
+    int lk_;     // params.lk (log2 of the sample streams)
+    // the running-mean weight of the lane's current sample within its stream (stream_weight)
     template <int F>
     __device__ __forceinline__ float w() const {
         if (!lane_lds(F)) return w_;
-        if (ft_none(F)) return 1.0f / (float)(reinterpret_cast<const int*>(acc)[11 * BLOCK] - first_ + 1);
+        if (ft_none(F)) return 1.0f / (float)(((reinterpret_cast<const int*>(acc)[11 * BLOCK] - first_) >> lk_) + 1);
         return acc[12 * BLOCK];
     }
 };
@@ -1339,37 +1341,22 @@ struct DAccum {
     float4* normal;
     long long* hits;
     unsigned long long* counters;  // 7 x u64: paths rays light_queries nodes instances prims shades;
-                                   // [7]: tile-order wait timeouts (must stay 0)
+                                   // [8..31]: the stamps build's per-phase clocks (JT_STAMPS)
     unsigned* work;                // unit counters of the launch, one per XCD band at work[16 b]
                                    // (zeroed before each launch)
-    int* tile_done;                // chunks accumulated in this launch: per 8x8 tile (trace_body) or per
-                                   // pixel slot tile * 64 + l (trace_body_items)
+    // sample-stream means (P.lk > 0): stream j of pixel p at [j * npix + p]; image RGBA, albedo
+    // xyz + the stream's hit count (int bits in w), normal xyz
+    float4* part_img;
+    float4* part_alb;
+    float4* part_nrm;
+    int npix;
 };
 
-// Work units: (sample chunk c, 8x8 pixel tile t), fetched by whole waves from atomic counters,
-// so every wave stays busy until the launch's last units. The tiles are split into 8 bands of
-// rows, one per XCD: a wave drains its own XCD's band first (neighbouring pixels share that
-// XCD's L2), then helps the other bands. Within a band units are numbered chunk-major, and a
-// tile's chunks run in order: a wave takes (c, t) only after (c - 1, t) has published its
-// running means (agent-scope release/acquire: a helper may run on another XCD).
+// Work units: (8x8 pixel tile t, stream slot q), fetched by whole waves from atomic counters, so
+// every wave stays busy until the launch's last units. The tiles are split into 8 bands of rows,
+// one per XCD: a wave drains its own XCD's band first (neighbouring pixels share that XCD's L2),
+// then helps the other bands. Within a band units are numbered stream-major.
 constexpr int NBANDS = 8, BAND_STRIDE = 16;
-__device__ __forceinline__ void wait_tile(const DAccum& A, int t, int c) {
-    if ((threadIdx.x & 63) == 0) {
-        int n = 0;
-        while (__hip_atomic_load(A.tile_done + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c) {
-            __builtin_amdgcn_s_sleep(8);
-            if (++n > (1 << 27)) {  // never expected (units are fetched in order): flag, do not hang
-                atomicAdd(A.counters + 7, 1ull);
-                break;
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-__device__ __forceinline__ void publish_tile(const DAccum& A, int t, int c) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if ((threadIdx.x & 63) == 0) __hip_atomic_store(A.tile_done + t, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // number of 8x8 tiles a launch covers (DParams tile_stride / tile_offset)
 __host__ __device__ __forceinline__ int launch_tiles(const DParams& P) {
@@ -1377,33 +1364,61 @@ __host__ __device__ __forceinline__ int launch_tiles(const DParams& P) {
     return all > P.tile_offset ? (all - P.tile_offset + P.tile_stride - 1) / P.tile_stride : 0;
 }
 
-// sample range of chunk uc of a launch over [s_begin, s_end)
-__device__ __forceinline__ int num_chunks(const DParams& P, int s_begin, int s_end) {
-    return P.nct > 0 ? P.nct : (s_end - s_begin + P.chunk - 1) / P.chunk;
+// ============================================================================ sample streams + per-lane work items
+// Sample streams: the samples of a pixel are dealt to k = 2^P.lk streams (local sample t = s -
+// first goes to stream t mod k), and each stream keeps its own running mean (src/trace.jl:631-648,
+// weight 1/(c + 1) for the stream's c-th sample). A (pixel, stream) item is one lane's work for
+// the launch: its samples in order, then one store of the stream's means. Items are independent
+// of each other — no item waits for another — so a launch has W·H·min(k, samples) concurrent
+// items however few pixels it covers, and the launch ends by combining each pixel's stream means
+// in stream order (combine_kernel, weights n_j / n). k = 1 is the reference's own single running
+// mean (the image buffer is stream 0). Results depend on k (fixed per context, jt_get_streams)
+// and not on how a render is split into calls or launches.
+//
+// Per-lane work items: the work units are (8x8 tile, stream), fetched by whole waves, but a lane
+// is not tied to its wave's unit: a lane that has finished its item takes the next pixel of its
+// wave's current unit at once, and the wave fetches the next unit when every pixel of the
+// current one has been handed out. A wave therefore never waits for the slowest lane of a unit;
+// lanes hold pixels of at most a few consecutive units, so neighbouring lanes stay spatially
+// close. The wave-level hand-out is a ballot and a prefix count (mbcnt): the k-th needy lane
+// takes pixel bnext + k.
+// JT_ITEM_FIRST_POP: a sample's first node pops run at its start, in the hand-out, where most of
+// the wave's lanes start samples together (1: every kernel, 0: none, 2: the binary-order mesh
+// kernels only). Measured in round 4 (profiles/r04_ab/knobs*_r04[rs].txt, two runs each), off
+// against on: cornellbox +0.4 % (10317/10318 vs 10273/10277 Mrays/s), bathroom1 and ecosys (wide)
+// +1.2 % and even, features2 (near, mesh) -1.5 % (2666/2679 vs 2722/2709). 2.
+#ifndef JT_ITEM_FIRST_POP
+#define JT_ITEM_FIRST_POP 2
+#endif
+template <bool WIDE, int F>
+__host__ __device__ constexpr bool item_first_pop() {
+    return JT_ITEM_FIRST_POP == 1 || (JT_ITEM_FIRST_POP == 2 && !WIDE && !ft_none(F));
 }
-__device__ __forceinline__ void chunk_range(const DParams& P, int s_begin, int s_end, int uc, int& cs0, int& cs1) {
-    if (P.nct > 0) {
-        cs0 = s_begin + P.cbeg[uc];
-        cs1 = s_begin + P.cbeg[uc + 1];
-    } else {
-        cs0 = s_begin + uc * P.chunk;
-        cs1 = cs0 + P.chunk < s_end ? cs0 + P.chunk : s_end;
-    }
+// a lane's item: the pixel's slot tile * 64 + l (l: pixel of the 8x8 tile; jt_create keeps
+// tiles below 2^20); ITEM_NONE: no pixel. The item's stream and sample live in the lane's LDS
+// slot [11] (its current global sample).
+constexpr unsigned ITEM_NONE = 0xffffffffu;
+
+// the image index of an item's pixel (its slot holds the global tile and the pixel of the tile)
+__device__ __forceinline__ int item_pixel(unsigned item, const DParams& P, int tiles_x) {
+    const int t = (int)(item >> 6), l = (int)(item & 63u);
+    return ((t / tiles_x) * 8 + (l >> 3)) * P.width + (t % tiles_x) * 8 + (l & 7);
+}
+// running-mean weight of global sample s within its stream
+__device__ __forceinline__ float stream_weight(const DParams& P, int s) {
+    return 1.0f / (float)(((s - P.first) >> P.lk) + 1);
 }
 
-// lane id (0..63) recomputed where it is used: an asm the compiler cannot merge with an earlier one
-__device__ __forceinline__ int opaque_lane_id() {
-    unsigned l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return (int)l;
-}
+#if JT_STAMPS
+#define JT_STAMP(x) x
+#else
+#define JT_STAMP(x)
+#endif
 
-// trace_samples over global samples [s_begin, s_end): one lane per pixel, 8x8-pixel wave tiles,
-// 16x16-pixel workgroups; a lane regenerates its path until its samples are done. The running
-// mean is read-modified-written per sample (src/trace.jl:631-648), in sample order.
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, bool WIDE>
-__device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, int s_begin, int s_end, const DAccum& A,
-                                           int* stack) {
+__device__ __forceinline__ void trace_body_items(const DScene& S, const DParams& P, int s_begin, int s_end,
+                                                 const DAccum& A, int* stack) {
+    static_assert(lane_lds(F), "the per-lane item body keeps the lane's sample index in LDS");
     const int lane = threadIdx.x & 63;
     const int oslot = (int)blockIdx.x * BLOCK + (int)threadIdx.x;  // the lane's HBM stack-overflow area
     if constexpr ((F & (FT_TEX | FT_ENV)) != 0) {  // the texel-decode LUTs into LDS (tex_lut)
@@ -1425,439 +1440,27 @@ __device__ __forceinline__ void trace_body(const DScene& S, const DParams& P, in
     auto lds_count = [&](int k, bool c) {
         if (c) __hip_atomic_fetch_add(wcnt + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    constexpr bool LL = lane_lds(F);
     __shared__ float acc_lds[acc_slots(F) * BLOCK];
     float* acc = acc_lds + threadIdx.x;
+    int* const acc_i = reinterpret_cast<int*>(acc);
 #if JT_STAMPS
+    // per-phase wave clocks, step lanes, shading-phase material coherence (scripts/stamps.py)
     unsigned long long t_trav = 0, t_shade = 0, n_trav = 0, n_shade = 0, lanes_p = 0, lanes_n = 0, steps_p = 0, steps_n = 0;
-    unsigned long long t_lhit = 0, t_phit = 0, t_fin = 0, t_qb = 0, n_lhit = 0, n_phit = 0, n_fin = 0;
-    unsigned long long dead_lanes = 0;  // lanes done with their unit's samples, per traversal iteration
-    // material coherence of the shading phases (what material sorting could gain): phases with
-    // surface hits to shade, and their summed distinct material types and material ids
-    unsigned long long n_mph = 0, n_mty = 0, n_mid = 0;
+    unsigned long long t_hit = 0, t_fin = 0, t_qb = 0, n_phit = 0, n_fin = 0, idle = 0, n_mph = 0, n_mty = 0, n_mid = 0;
+    unsigned long long lanes_sh = 0, lanes_hit = 0, t_start = 0, n_start = 0, lanes_start = 0;
 #endif
-    // this launch's tiles: every tile_stride-th from tile_offset (all of them on one device)
     const int tiles_x = (P.width + 7) / 8, tiles = launch_tiles(P);
-    const int nchunks = num_chunks(P, s_begin, s_end);
+    const int kstr = 1 << P.lk;
+    // stream slots of this launch: q = 0 .. nq-1 starts at global sample s_begin + q
+    const int nq = s_end - s_begin < kstr ? s_end - s_begin : kstr;
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     int band_k = 0;
-    for (;;) {
-    const int band = (int)((xcc + (unsigned)band_k) & (NBANDS - 1));
-    const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
-    unsigned unit = 0;
-    if (lane == 0) unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
-    unit = __builtin_amdgcn_readfirstlane(unit);
-    if (unit >= (unsigned)bn * (unsigned)nchunks) {  // this band is drained: help the next one
-        if (++band_k >= NBANDS) break;
-        continue;
-    }
-    const int uc = (int)(unit / (unsigned)bn), ut = (bt0 + (int)(unit % (unsigned)bn)) * P.tile_stride + P.tile_offset;
-    if (uc > 0) wait_tile(A, ut, uc);
-    const int i = (ut % tiles_x) * 8 + (lane & 7);
-    const int j = (ut / tiles_x) * 8 + (lane >> 3);
-    int cs0, cs1;
-    chunk_range(P, s_begin, s_end, uc, cs0, cs1);
-    int pixel = j * P.width + i;
-    bool in_image = i < P.width && j < P.height;
-    bool alive = in_image;
-    int sample = cs0;
-    if (in_image) {
-        const float4 im = A.image[pixel], al = A.albedo[pixel], nr = A.normal[pixel];
-        acc[0] = im.x;
-        acc[BLOCK] = im.y;
-        acc[2 * BLOCK] = im.z;
-        acc[3 * BLOCK] = im.w;
-        acc[4 * BLOCK] = al.x;
-        acc[5 * BLOCK] = al.y;
-        acc[6 * BLOCK] = al.z;
-        acc[7 * BLOCK] = nr.x;
-        acc[8 * BLOCK] = nr.y;
-        acc[9 * BLOCK] = nr.z;
-        reinterpret_cast<int*>(acc)[10 * BLOCK] = 0;
-    }
-    int* const acc_i = reinterpret_cast<int*>(acc);
-    Aov aov{acc, 0.0f, P.first};
-    if (LL) {
-        if (in_image) {
-            acc_i[11 * BLOCK] = sample;
-            if (!ft_none(F)) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
-        }
-    } else {
-        aov.w_ = 1.0f / (float)(sample - P.first + 1);
-    }
-    Path st;
-    st.pk = acc + acc_base_slots(F) * BLOCK;
-    Trav T;
-    // lane states, from the stack cursor alone: sp < 0 finished (no samples left), nprim > 0 or
-    // sp > 0 in a query, sp == nprim == 0 waiting for the shading phase
-    T.sp = -1;
-    T.nprim = 0;
-    T.nxt = W_EMPTY;
-    if (alive) {
-        start_path<F>(P, i, j, pixel, sample, st);
-        query_start<WIDE>(S, T, st.o, st.d, -1, stack);
-    }
-    if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(alive));
-    else lds_count(1, alive);
-    for (;;) {
-#if JT_STAMPS
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
-        // traversal phase: step every lane with a query in flight until at least W lanes wait
-        // Each iteration runs ONE step kind — primitive tests or stack pops — picked by lane
-        // majority (a wave-uniform branch), so the SIMD executes one code path per iteration.
-        // A lane's own sequence of steps is unchanged: it only waits while the other kind runs.
-        // Light-hit steps (path sampler, scenes without environments, whose light_hit is short):
-        // a lane whose sample_lights_pdf query has finished does not wait for the shading
-        // phase — once enough such lanes gather (or nothing else is left to step) the wave runs
-        // light_hit on them and their next query starts at once.
-        constexpr bool LSTEP = light_steps(SAMPLER, F);
-        for (;;) {
-            const bool wantp = T.nprim > 0;
-            const bool wantn = wants_node<WIDE>(T);
-            const bool waiting = query_done<WIDE>(T);
-            const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
-            const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
-            int nw = lane_count(__builtin_amdgcn_ballot_w64(waiting));
-            const int nb = np + nn;
-            if (LSTEP && !S.light_inline) {  // light chains run inline: none waits in PH_LIGHT
-                const bool wantl = waiting && st.phase == PH_LIGHT;
-                const int nl = lane_count(__builtin_amdgcn_ballot_w64(wantl));
-                if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
-                    bool c_lq = false, c_ray = false;
-                    if (wantl) {
-                        if (light_hit<F>(S, P, st, query_hit(T))) {
-                            st.phase = PH_FINISH;
-                        } else if (st.phase == PH_LIGHT) {
-                            if (WC) c_lq = true;
-                            else lds_count(2, true);
-                            query_start<WIDE>(S, T, st.o, st.d, S.lights[st.li].instance, stack);
-                        } else {
-                            if (WC) c_ray = true;
-                            else lds_count(1, true);
-                            query_start<WIDE>(S, T, st.o, st.d, -1, stack);
-                        }
-                    }
-                    if (WC) {
-                        w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
-                        w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
-                    }
-                    continue;
-                }
-                nw -= nl;
-            }
-            if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
-#if JT_STAMPS
-            n_trav++;
-            dead_lanes += 64 - lane_count(__builtin_amdgcn_ballot_w64(T.sp >= 0));
-            if (np >= nn) { steps_p++; lanes_p += np; } else { steps_n++; lanes_n += nn; }
-#endif
-            if (JT_RAY_FROM_PATH && !(F & FT_XFORM)) {
-                // without instance transforms a query's ray is its path's (st.o, st.d), unchanged
-                // while the query runs: re-reading it here keeps one copy, not two, live across
-                // the loop (register renaming only, no instructions)
-                T.lo = st.o;
-                T.ld = st.d;
-            }
-            if (np * JT_VOTE_P >= nn * JT_VOTE_N) {
-                if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-            } else {
-                // JT_NODE_REPEAT pops per node iteration: a lane whose next step is again a
-                // stack pop takes it at once (the same steps in the same per-lane order, less
-                // per-iteration vote and loop overhead)
-                constexpr int NREP = ft_none(F) ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
-#pragma unroll
-                for (int k = 0; k < NREP; k++)
-                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
-            }
-        }
-#if JT_STAMPS
-        unsigned long long t1 = __builtin_amdgcn_s_memtime();
-        t_trav += t1 - t0;
-        n_shade++;
-#endif
-        // shading phase: every waiting lane consumes its hit and issues its next query
-        bool c_path = false, c_lq = false, c_ray = false;
-        unsigned n_inl = 0;  // WC: this lane's inline light queries (light_chain)
-#if JT_STAMPS
-        {
-            int mid = -1, mt = -1;
-            if (query_done<WIDE>(T) && st.phase == PH_SCENE && T.h_inst >= 0) {
-                mid = S.inst_shade[T.h_inst].material;
-                mt = (F & FT_MAT) ? S.materials[mid].type : (int)M_MATTE;
-            }
-            if (__ballot(mt >= 0)) {
-                n_mph++;
-                for (int ty = 0; ty <= (int)M_GLTFPBR; ty++) n_mty += __ballot(mt == ty) ? 1u : 0u;
-                bool counted = mt < 0;
-                for (;;) {
-                    const unsigned long long m = __ballot(!counted);
-                    if (!m) break;
-                    const int v = __shfl(mid, __ffsll((long long)m) - 1);
-                    counted = counted || mid == v;
-                    n_mid++;
-                }
-            }
-        }
-#endif
-        if (query_done<WIDE>(T)) {
-            bool alive = true;
-            // no light query ever leaves the shading phase (FT_LINL), or none exists (FT_NOIL)
-            constexpr bool LINL = (F & (FT_LINL | FT_NOIL)) != 0;
-            const bool light = SAMPLER == 1 && !LINL && st.phase == PH_LIGHT;
-            bool done;
-#if JT_STAMPS
-            unsigned long long s0 = __builtin_amdgcn_s_memtime();
-            if (light) done = light_hit<F>(S, P, st, query_hit(T));
-            unsigned long long s1 = __builtin_amdgcn_s_memtime();
-            if (LSTEP && st.phase == PH_FINISH) done = true;
-            else if (!light) {
-                if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
-                else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
-            }
-            unsigned long long s2 = __builtin_amdgcn_s_memtime();
-            if (__ballot(light)) { t_lhit += s1 - s0; n_lhit++; }
-            if (__ballot(!light)) { t_phit += s2 - s1; n_phit++; }
-            if (__ballot(done)) n_fin++;
-#else
-            if (LSTEP && st.phase == PH_FINISH) done = true;
-            else if (light) done = light_hit<F>(S, P, st, query_hit(T));
-            else if (SAMPLER == 2) done = naive_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
-            else done = path_hit<F>(S, P, st, query_hit(T), aov, cnt.shades);
-#endif
-            if (SAMPLER == 1 && !done && st.phase == PH_LIGHT && chains_inline(F, S)) {
-                unsigned nlq = 0;
-                done = light_chain<WIDE, RING, OVF, COUNT, NCACHE, F>(S, P, st, T, stack, oslot, cnt, [&] {
-                    if (WC) nlq++;
-                    else lds_count(2, true);
-                });
-                if (WC) n_inl += nlq;
-            }
-            if (done) {
-                // trace_sample epilogue (src/trace.jl:625-648)
-                if (WC) c_path = true;
-                else lds_count(0, true);
-                v3 radiance = st.radiance<F>();
-                if (!all_finite(radiance)) radiance = V3(0, 0, 0);
-                const float mr = max3(radiance);
-                if (mr > P.clamp) radiance = radiance * (P.clamp / mr);
-                const float w = aov.w<F>();
-                const float omw = 1 - w;
-                const bool hit = st.flag(F_HIT);
-                const bool env = !hit && !P.envhidden && S.nenvs != 0;
-                const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
-                // no bounce-0 surface was accepted: st.d is still the camera ray direction
-                if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
-                acc[0] = acc[0] * omw + target.x * w;
-                acc[BLOCK] = acc[BLOCK] * omw + target.y * w;
-                acc[2 * BLOCK] = acc[2 * BLOCK] * omw + target.z * w;
-                acc[3 * BLOCK] = acc[3 * BLOCK] * omw + target.w * w;
-                if (hit || env) reinterpret_cast<int*>(acc)[10 * BLOCK] += 1;
-                if constexpr (LL) {
-                // the pixel from the unit's wave-uniform tile and a lane id the compiler cannot
-                // reuse from the top of the unit, so i / j do not stay live across the loop
-                const int sample = acc_i[11 * BLOCK] + 1;
-                if (sample >= cs1) {
-                    alive = false;
-                    T.sp = -1;
-                } else {
-                    acc_i[11 * BLOCK] = sample;
-                    if (!ft_none(F)) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
-                    const int lx = opaque_lane_id();
-                    const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
-                    start_path<F>(P, i2, j2, j2 * P.width + i2, sample, st);
-                }
-                } else {
-                if (++sample >= cs1) {
-                    alive = false;
-                    T.sp = -1;
-                } else {
-                    aov.w_ = 1.0f / (float)(sample - P.first + 1);
-                    start_path<F>(P, i, j, pixel, sample, st);
-                }
-                }
-            }
-#if JT_STAMPS
-            unsigned long long s3 = __builtin_amdgcn_s_memtime();
-            t_fin += s3 - s2;
-#endif
-            if (alive) {
-                if (SAMPLER == 1 && !LINL && st.phase == PH_LIGHT) {
-                    if (WC) c_lq = true;
-                    else lds_count(2, true);
-                    query_start<WIDE>(S, T, st.o, st.d, S.lights[st.li].instance, stack);
-                } else {
-                    if (WC) c_ray = true;
-                    else lds_count(1, true);
-                    query_start<WIDE>(S, T, st.o, st.d, -1, stack);
-                }
-                // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
-                // where most of the wave's lanes take part, rather than in a sparser traversal step
-#pragma unroll
-                for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
-                    if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
-            }
-#if JT_STAMPS
-            t_qb += __builtin_amdgcn_s_memtime() - s3;
-#endif
-        }
-#if JT_STAMPS
-        t_shade += __builtin_amdgcn_s_memtime() - t1;
-#endif
-        if (WC) {
-            w_paths += lane_count(__builtin_amdgcn_ballot_w64(c_path));
-            w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
-            w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
-            if (SAMPLER == 1 && chains_inline(F, S)) w_lq += __builtin_amdgcn_readfirstlane(wave_sum(n_inl));
-        }
-        if (__ballot(T.sp >= 0) == 0) break;
-    }
-    if constexpr (LL) {
-        const int lx = opaque_lane_id();
-        const int i2 = (ut % tiles_x) * 8 + (lx & 7), j2 = (ut / tiles_x) * 8 + (lx >> 3);
-        pixel = j2 * P.width + i2;
-        in_image = i2 < P.width && j2 < P.height;
-    }
-    if (in_image) {
-        A.image[pixel] = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);
-        A.albedo[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
-        A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
-        A.hits[pixel] += reinterpret_cast<const int*>(acc)[10 * BLOCK];
-    }
-    if (uc + 1 < nchunks) publish_tile(A, ut, uc);
-    }  // units
-#if JT_STAMPS
-    if (lane == 0) {
-        unsigned long long* dbg = A.counters + 8;
-        atomicAdd(dbg + 0, t_trav);
-        atomicAdd(dbg + 1, t_shade);
-        atomicAdd(dbg + 2, n_trav);
-        atomicAdd(dbg + 3, n_shade);
-        atomicAdd(dbg + 4, lanes_p);
-        atomicAdd(dbg + 5, lanes_n);
-        atomicAdd(dbg + 6, steps_p);
-        atomicAdd(dbg + 7, steps_n);
-        atomicAdd(dbg + 8, t_lhit);
-        atomicAdd(dbg + 9, t_phit);
-        atomicAdd(dbg + 10, t_fin);
-        atomicAdd(dbg + 11, t_qb);
-        atomicAdd(dbg + 12, n_lhit);
-        atomicAdd(dbg + 13, n_phit);
-        atomicAdd(dbg + 14, n_fin);
-        atomicAdd(dbg + 15, dead_lanes);
-        atomicAdd(dbg + 16, n_mph);
-        atomicAdd(dbg + 17, n_mty);
-        atomicAdd(dbg + 18, n_mid);
-    }
-#endif
-    // one atomic per counter per wave (the wave's own LDS adds precede this read in program order)
-    const unsigned wv[3] = {w_paths, w_rays, w_lq};
-    unsigned v[7] = {0u, 0u, 0u, cnt.nodes, cnt.instances, cnt.prims, COUNT ? cnt.shades : 0u};
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-        unsigned s = k < 3 ? (WC ? wv[k] : wcnt[k]) : wave_sum(v[k]);
-        if (lane == 0 && s) atomicAdd(&A.counters[k], (unsigned long long)s);
-    }
-}
-
-// ============================================================================ per-lane work items
-// JT_LANE_ITEMS: the work units stay (8x8 tile t, sample chunk c), fetched by whole waves, but a
-// lane is no longer tied to its wave's unit: a lane that has finished its pixel's chunk takes the
-// next pixel of its wave's current unit at once, and the wave fetches the next unit when every
-// pixel of the current one has been handed out. A wave therefore never waits for the slowest
-// lane of a unit (the "dead lanes" of DESIGN.md §2); lanes hold pixels of at most a few
-// consecutive units, so neighbouring lanes stay spatially close. The wave-level hand-out is a
-// ballot and a prefix count (mbcnt): lane k of the needy lanes takes pixel bnext + k.
-// A pixel's chunks still run in order (the running mean is order-dependent, src/trace.jl:631-648):
-// a lane that takes (c, pixel) with c > 0 starts once (c - 1, pixel) is published, which is by
-// then almost always the case (units are numbered chunk-major). The hand-off of one pixel's
-// running means between lanes — possibly on another CU or XCD — is write-through: the finishing
-// lane stores them with sc1 stores (agent-scope relaxed atomics, 8 B each), the wave drains its
-// stores (s_waitcnt vmcnt(0)), then the lane stores the pixel's done word; the taking lane polls
-// that word (relaxed agent load) and reads the means with sc1 loads, so no cache-wide fence is
-// needed (cdna_hip_programming.md Guideline 16, write-through hand-off). A lane whose pixel is not
-// ready yet does not spin: it is re-checked every iteration while the other lanes work.
-// Results are bit-identical: every pixel's samples run in order with the same float operations.
-#ifndef JT_LANE_ITEMS
-#define JT_LANE_ITEMS 1
-#endif
-// JT_ITEM_FIRST_POP: a sample's first node pops run at its start, in the hand-out, where most of
-// the wave's lanes start samples together (1: every kernel, 0: none, 2: the binary-order mesh
-// kernels only). Measured in round 4 (profiles/r04_ab/knobs*_r04[rs].txt, two runs each), off
-// against on: cornellbox +0.4 % (10317/10318 vs 10273/10277 Mrays/s), bathroom1 and ecosys (wide)
-// +1.2 % and even, features2 (near, mesh) -1.5 % (2666/2679 vs 2722/2709). 2.
-#ifndef JT_ITEM_FIRST_POP
-#define JT_ITEM_FIRST_POP 2
-#endif
-template <bool WIDE, int F>
-__host__ __device__ constexpr bool item_first_pop() {
-    return JT_ITEM_FIRST_POP == 1 || (JT_ITEM_FIRST_POP == 2 && !WIDE && !ft_none(F));
-}
-// a lane's item: bits 0-25 the pixel's slot tile * 64 + l (l: pixel of the 8x8 tile; jt_create
-// keeps tiles below 2^20), 26-30 its chunk, 31 ITEM_BLOCKED (taken, waiting for the previous
-// chunk of the pixel); ITEM_NONE: no pixel
-constexpr unsigned ITEM_NONE = 0xffffffffu, ITEM_BLOCKED = 0x80000000u, ITEM_SLOT_MASK = (1u << 26) - 1u;
-constexpr int ITEM_CHUNK_SHIFT = 26;
-__device__ __forceinline__ int item_chunk(unsigned item) { return (int)((item >> ITEM_CHUNK_SHIFT) & 31u); }
-__device__ __forceinline__ unsigned long long ld_sc1(const void* p) {
-    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(void* p, unsigned long long v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long pack2(float a, float b) {
-    return (unsigned long long)__float_as_uint(a) | (unsigned long long)__float_as_uint(b) << 32;
-}
-__device__ __forceinline__ float lo_f(unsigned long long v) { return __uint_as_float((unsigned)v); }
-__device__ __forceinline__ float hi_f(unsigned long long v) { return __uint_as_float((unsigned)(v >> 32)); }
-
-// the image index of an item's pixel (its slot holds the global tile and the pixel of the tile)
-__device__ __forceinline__ int item_pixel(unsigned item, const DParams& P, int tiles_x) {
-    const int slot = (int)(item & ITEM_SLOT_MASK), t = slot >> 6, l = slot & 63;
-    return ((t / tiles_x) * 8 + (l >> 3)) * P.width + (t % tiles_x) * 8 + (l & 7);
-}
-template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, bool WIDE>
-__device__ __forceinline__ void trace_body_items(const DScene& S, const DParams& P, int s_begin, int s_end,
-                                                 const DAccum& A, int* stack) {
-    static_assert(lane_lds(F), "the per-lane item body keeps the lane's sample index in LDS");
-    const int lane = threadIdx.x & 63;
-    const int oslot = (int)blockIdx.x * BLOCK + (int)threadIdx.x;  // the lane's HBM stack-overflow area
-    if constexpr ((F & (FT_TEX | FT_ENV)) != 0) {  // the texel-decode LUTs into LDS (tex_lut)
-        for (int k = threadIdx.x; k < 512; k += BLOCK) tex_lut[k] = k < 256 ? S.srgb_lut[k] : S.byte_lut[k - 256];
-    }
-    // chunk boundaries in LDS: a lane's chunk is per lane here, so its end is looked up per lane
-    __shared__ int cb_lds[JT_MAX_CHUNKS + 2];
-    for (int k = threadIdx.x; k < JT_MAX_CHUNKS + 2; k += BLOCK) {
-        int a, b;
-        if (k < num_chunks(P, s_begin, s_end)) chunk_range(P, s_begin, s_end, k, a, b);
-        else a = b = s_end;
-        cb_lds[k] = b;  // end of chunk k
-    }
-    __syncthreads();
-    Counters cnt{0, 0, 0, 0};
-    constexpr bool WC = !ft_none(F);
-    unsigned w_paths = 0, w_rays = 0, w_lq = 0;
-    __shared__ unsigned wave_cnt[WC ? 1 : (BLOCK / 64) * 4];
-    unsigned* const wcnt = wave_cnt + (WC ? 0 : (threadIdx.x >> 6) * 4);
-    if (!WC && lane < 3) wcnt[lane] = 0u;
-    auto lds_count = [&](int k, bool c) {
-        if (c) __hip_atomic_fetch_add(wcnt + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    __shared__ float acc_lds[acc_slots(F) * BLOCK];
-    float* acc = acc_lds + threadIdx.x;
-    int* const acc_i = reinterpret_cast<int*>(acc);
-    const int tiles_x = (P.width + 7) / 8, tiles = launch_tiles(P);
-    const int nchunks = num_chunks(P, s_begin, s_end);
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    int band_k = 0;
-    int ut = 0, uc = 0, bnext = 64;  // the wave's current unit (tile, chunk) and its next pixel to hand out
+    int ut = 0, uq = 0, bnext = 64;  // the wave's current unit (tile, stream slot) and its next pixel to hand out
     bool drained = false;            // every band's units handed out
     unsigned item = ITEM_NONE;       // the lane's pixel (ITEM_* above)
-    int spins = 0;                   // iterations in which every held pixel waited (bounded)
     bool next_sample = false;        // the lane's next sample starts at the top of the iteration
-    Aov aov{acc, 0.0f, P.first};
+    Aov aov{acc, 0.0f, P.first, P.lk};
     Path st;
     st.pk = acc + acc_base_slots(F) * BLOCK;
     Trav T;
@@ -1865,7 +1468,10 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
     T.nprim = 0;
     T.nxt = W_EMPTY;
     for (;;) {
-        // ---- hand out pixels to the lanes without one (wave-uniform control)
+        JT_STAMP(const unsigned long long ts0 = __builtin_amdgcn_s_memtime());
+        // ---- hand out pixels to the lanes without one (wave-uniform control); a lane taking an
+        // item starts from its stream's means so far (zero for the stream's first sample)
+        bool start = next_sample;
         for (;;) {
             const unsigned long long needm = __builtin_amdgcn_ballot_w64(item == ITEM_NONE);
             if (!needm || drained) break;
@@ -1875,11 +1481,11 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 unsigned unit = 0;
                 if (lane == 0) unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
                 unit = __builtin_amdgcn_readfirstlane(unit);
-                if (unit >= (unsigned)bn * (unsigned)nchunks) {
+                if (unit >= (unsigned)bn * (unsigned)nq) {
                     if (++band_k >= NBANDS) drained = true;
                     continue;
                 }
-                uc = (int)(unit / (unsigned)bn);
+                uq = (int)(unit / (unsigned)bn);
                 ut = (bt0 + (int)(unit % (unsigned)bn)) * P.tile_stride + P.tile_offset;
                 bnext = 0;
             }
@@ -1889,44 +1495,50 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 const int l = bnext + rank;
                 const int i = (ut % tiles_x) * 8 + (l & 7), j = (ut / tiles_x) * 8 + (l >> 3);
                 // a pixel outside the image (edge tiles) is skipped: the lane takes another
-                if (i < P.width && j < P.height) item = (unsigned)(ut * 64 + l) | (unsigned)uc << ITEM_CHUNK_SHIFT | ITEM_BLOCKED;
+                if (i < P.width && j < P.height) {
+                    item = (unsigned)(ut * 64 + l);
+                    start = true;
+                    const int s = s_begin + uq;
+                    acc_i[11 * BLOCK] = s;
+                    const int pixel = j * P.width + i;
+                    float4 im = make_float4(0, 0, 0, 0), al = im, nr = im;
+                    int h = 0;
+                    if (s - P.first >= kstr) {  // the stream has earlier samples (an earlier launch)
+                        if (P.lk == 0) {
+                            im = A.image[pixel];
+                            al = A.albedo[pixel];
+                            nr = A.normal[pixel];
+                            h = (int)A.hits[pixel];
+                        } else {
+                            const size_t o = (size_t)((s - P.first) & (kstr - 1)) * (size_t)A.npix + (size_t)pixel;
+                            im = A.part_img[o];
+                            al = A.part_alb[o];
+                            nr = A.part_nrm[o];
+                            h = __float_as_int(al.w);
+                        }
+                    }
+                    acc[0] = im.x;
+                    acc[BLOCK] = im.y;
+                    acc[2 * BLOCK] = im.z;
+                    acc[3 * BLOCK] = im.w;
+                    acc[4 * BLOCK] = al.x;
+                    acc[5 * BLOCK] = al.y;
+                    acc[6 * BLOCK] = al.z;
+                    acc[7 * BLOCK] = nr.x;
+                    acc[8 * BLOCK] = nr.y;
+                    acc[9 * BLOCK] = nr.z;
+                    acc_i[10 * BLOCK] = h;
+                }
             }
             bnext += take;
         }
-        // ---- lanes whose pixel's previous chunk is published take it: running means from HBM
-        // (sc1 loads), the chunk's first sample
-        bool start = next_sample;
-        if (item != ITEM_NONE && (item & ITEM_BLOCKED)) {
-            const int c = item_chunk(item);
-            if (c == 0 || spins > (1 << 22) ||
-                __hip_atomic_load(A.tile_done + (item & ITEM_SLOT_MASK), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c) {
-                start = true;
-                item &= ~ITEM_BLOCKED;
-                const int pixel = item_pixel(item, P, tiles_x);
-                const unsigned long long i0 = ld_sc1(&A.image[pixel].x), i1 = ld_sc1(&A.image[pixel].z);
-                const unsigned long long a0 = ld_sc1(&A.albedo[pixel].x), a1 = ld_sc1(&A.albedo[pixel].z);
-                const unsigned long long n0 = ld_sc1(&A.normal[pixel].x), n1 = ld_sc1(&A.normal[pixel].z);
-                acc[0] = lo_f(i0);
-                acc[BLOCK] = hi_f(i0);
-                acc[2 * BLOCK] = lo_f(i1);
-                acc[3 * BLOCK] = hi_f(i1);
-                acc[4 * BLOCK] = lo_f(a0);
-                acc[5 * BLOCK] = hi_f(a0);
-                acc[6 * BLOCK] = lo_f(a1);
-                acc[7 * BLOCK] = lo_f(n0);
-                acc[8 * BLOCK] = hi_f(n0);
-                acc[9 * BLOCK] = lo_f(n1);
-                acc_i[10 * BLOCK] = 0;
-                acc_i[11 * BLOCK] = c == 0 ? s_begin : cb_lds[c - 1];
-            }
-        }
-        // ---- every lane starting a sample (a new pixel, or the next sample of its pixel): the
+        // ---- every lane starting a sample (a new item, or the next sample of its stream): the
         // camera ray (trace_sample's prologue) and its query's first pops, where many lanes share them
         next_sample = false;
         if (start) {
             const int sample = acc_i[11 * BLOCK];
             const int pixel = item_pixel(item, P, tiles_x);
-            if (!ft_none(F)) acc[12 * BLOCK] = 1.0f / (float)(sample - P.first + 1);
+            if (!ft_none(F)) acc[12 * BLOCK] = stream_weight(P, sample);
             start_path<F>(P, pixel % P.width, pixel / P.width, pixel, sample, st);
             query_start<WIDE>(S, T, st.o, st.d, -1, stack);
             if (!WC) lds_count(1, true);
@@ -1937,17 +1549,19 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
             }
         }
         if (WC) w_rays += lane_count(__builtin_amdgcn_ballot_w64(start));
+#if JT_STAMPS
+        const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+        t_start += ts1 - ts0;
+        n_start++;
+        lanes_start += lane_count(__builtin_amdgcn_ballot_w64(start));
+#endif
         if (__builtin_amdgcn_ballot_w64(item != ITEM_NONE) == 0) break;  // drained, and every lane is done
-        if (__builtin_amdgcn_ballot_w64(item != ITEM_NONE && !(item & ITEM_BLOCKED)) == 0) {
-            // every pixel held waits for its previous chunk (never expected: units are handed out
-            // chunk-major). Bounded: past the bound the wave flags the launch (counters[7], the
-            // host then fails it with JT_ERR_DEVICE) and starts the pixels rather than hang.
-            // (No `continue` here: a second back-edge of the loop made the register allocator
-            // spill 44-68 VGPRs of path state; with no lane active the phases below are no-ops.)
-            if (++spins == (1 << 22) && lane == 0) atomicAdd(A.counters + 7, 1ull);
-            __builtin_amdgcn_s_sleep(8);
-        }
-        // ---- traversal phase (as trace_body)
+        // ---- traversal phase: step every lane with a query in flight until enough lanes wait.
+        // Each iteration runs ONE step kind — primitive tests or stack pops — picked by a biased
+        // lane vote (a wave-uniform branch), so the SIMD executes one code path per iteration; a
+        // lane's own sequence of steps is unchanged, it only waits while the other kind runs.
+        // Light-hit steps (path sampler, matte scenes whose light chains cannot run inline): a
+        // lane whose sample_lights_pdf query has finished does not wait for the shading phase.
         constexpr bool LSTEP = light_steps(SAMPLER, F);
         for (;;) {
             const bool wantp = T.nprim > 0;
@@ -1984,24 +1598,63 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 nw -= nl;
             }
             if (nb == 0 || nw >= (nb + nw < P.wait_lanes ? nb + nw : P.wait_lanes)) break;
+#if JT_STAMPS
+            n_trav++;
+            idle += 64 - lane_count(__builtin_amdgcn_ballot_w64(item != ITEM_NONE));
+            if (np * JT_VOTE_P >= nn * JT_VOTE_N) { steps_p++; lanes_p += np; } else { steps_n++; lanes_n += nn; }
+#endif
             if (JT_RAY_FROM_PATH && !(F & FT_XFORM)) {
+                // without instance transforms a query's ray is its path's (st.o, st.d), unchanged
+                // while the query runs: re-reading it here keeps one copy, not two, live across
+                // the loop (register renaming only, no instructions)
                 T.lo = st.o;
                 T.ld = st.d;
             }
             if (np * JT_VOTE_P >= nn * JT_VOTE_N) {
                 if (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
             } else {
+                // JT_NODE_REPEAT pops per node iteration: a lane whose next step is again a
+                // stack pop takes it at once (the same steps in the same per-lane order, less
+                // per-iteration vote and loop overhead)
                 constexpr int NREP = ft_none(F) ? JT_NODE_REPEAT_NONE : JT_NODE_REPEAT;
 #pragma unroll
                 for (int k = 0; k < NREP; k++)
                     if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
             }
         }
+#if JT_STAMPS
+        const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
+        t_trav += ts2 - ts1;
+        n_shade++;
+        lanes_sh += lane_count(__builtin_amdgcn_ballot_w64(query_done<WIDE>(T)));
+        {
+            int mid = -1, mt = -1;
+            if (query_done<WIDE>(T) && st.phase == PH_SCENE && T.h_inst >= 0) {
+                mid = S.inst_shade[T.h_inst].material;
+                mt = (F & FT_MAT) ? S.materials[mid].type : (int)M_MATTE;
+            }
+            if (__builtin_amdgcn_ballot_w64(mt >= 0)) {
+                n_mph++;
+                lanes_hit += lane_count(__builtin_amdgcn_ballot_w64(mt >= 0));
+                for (int ty = 0; ty <= (int)M_GLTFPBR; ty++) n_mty += __builtin_amdgcn_ballot_w64(mt == ty) ? 1u : 0u;
+                bool counted = mt < 0;
+                for (;;) {
+                    const unsigned long long m = __builtin_amdgcn_ballot_w64(!counted);
+                    if (!m) break;
+                    const int v = __shfl(mid, __ffsll((long long)m) - 1);
+                    counted = counted || mid == v;
+                    n_mid++;
+                }
+            }
+        }
+        unsigned long long ts3 = ts2, ts4 = ts2;
+#endif
         // ---- shading phase: every waiting lane consumes its hit and issues its next query
-        bool c_path = false, c_lq = false, c_ray = false, c_done = false;
+        bool c_path = false, c_lq = false, c_ray = false;
         unsigned n_inl = 0;
         if (query_done<WIDE>(T)) {
             bool alive = true;
+            // no light query ever leaves the shading phase (FT_LINL), or none exists (FT_NOIL)
             constexpr bool LINL = (F & (FT_LINL | FT_NOIL)) != 0;
             const bool light = SAMPLER == 1 && !LINL && st.phase == PH_LIGHT;
             bool done;
@@ -2017,8 +1670,12 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 });
                 if (WC) n_inl += nlq;
             }
+#if JT_STAMPS
+            ts3 = __builtin_amdgcn_s_memtime();
+            n_phit++;
+#endif
             if (done) {
-                // trace_sample epilogue (src/trace.jl:625-648)
+                // trace_sample epilogue (src/trace.jl:625-648), into the item's stream mean
                 if (WC) c_path = true;
                 else lds_count(0, true);
                 v3 radiance = st.radiance<F>();
@@ -2030,34 +1687,42 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 const bool hit = st.flag(F_HIT);
                 const bool env = !hit && !P.envhidden && S.nenvs != 0;
                 const v4 target = (hit || env) ? V4(radiance.x, radiance.y, radiance.z, 1) : V4(0, 0, 0, 0);
+                // no bounce-0 surface was accepted: st.d is still the camera ray direction
                 if (!hit) aov_update<F>(aov, env ? V3(1, 1, 1) : V3(0, 0, 0), -st.d);
                 acc[0] = acc[0] * omw + target.x * w;
                 acc[BLOCK] = acc[BLOCK] * omw + target.y * w;
                 acc[2 * BLOCK] = acc[2 * BLOCK] * omw + target.z * w;
                 acc[3 * BLOCK] = acc[3 * BLOCK] * omw + target.w * w;
                 if (hit || env) acc_i[10 * BLOCK] += 1;
-                const int sample = acc_i[11 * BLOCK] + 1;
-                if (sample >= cb_lds[item_chunk(item)]) {
-                    // the pixel's chunk is complete: write-through its running means, hits at the memory side
-                    alive = false;
-                    T.sp = -1;
+                alive = false;
+                T.sp = -1;
+                const int sample = acc_i[11 * BLOCK];
+                if (sample + kstr >= s_end) {
+                    // the item is complete: store its stream's means (plain stores: no other item
+                    // of this launch reads them; the combine kernel runs after the launch)
                     const int pixel = item_pixel(item, P, tiles_x);
-                    st_sc1(&A.image[pixel].x, pack2(acc[0], acc[BLOCK]));
-                    st_sc1(&A.image[pixel].z, pack2(acc[2 * BLOCK], acc[3 * BLOCK]));
-                    st_sc1(&A.albedo[pixel].x, pack2(acc[4 * BLOCK], acc[5 * BLOCK]));
-                    st_sc1(&A.albedo[pixel].z, pack2(acc[6 * BLOCK], 0.0f));
-                    st_sc1(&A.normal[pixel].x, pack2(acc[7 * BLOCK], acc[8 * BLOCK]));
-                    st_sc1(&A.normal[pixel].z, pack2(acc[9 * BLOCK], 0.0f));
-                    if (acc_i[10 * BLOCK]) atomicAdd(reinterpret_cast<unsigned long long*>(A.hits + pixel),
-                                                     (unsigned long long)acc_i[10 * BLOCK]);
-                    c_done = true;
+                    const float4 im = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);
+                    if (P.lk == 0) {
+                        A.image[pixel] = im;
+                        A.albedo[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
+                        A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
+                        A.hits[pixel] = (long long)acc_i[10 * BLOCK];
+                    } else {
+                        const size_t o = (size_t)((sample - P.first) & (kstr - 1)) * (size_t)A.npix + (size_t)pixel;
+                        A.part_img[o] = im;
+                        A.part_alb[o] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], __int_as_float(acc_i[10 * BLOCK]));
+                        A.part_nrm[o] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
+                    }
+                    item = ITEM_NONE;
                 } else {
-                    acc_i[11 * BLOCK] = sample;  // started at the top of the next iteration
-                    alive = false;
-                    T.sp = -1;
+                    acc_i[11 * BLOCK] = sample + kstr;  // started at the top of the next iteration
                     next_sample = true;
                 }
             }
+#if JT_STAMPS
+            ts4 = __builtin_amdgcn_s_memtime();
+            if (__builtin_amdgcn_ballot_w64(done)) n_fin++;
+#endif
             if (alive) {
                 if (SAMPLER == 1 && !LINL && st.phase == PH_LIGHT) {
                     if (WC) c_lq = true;
@@ -2068,28 +1733,37 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                     else lds_count(1, true);
                     query_start<WIDE>(S, T, st.o, st.d, -1, stack);
                 }
+                // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
+                // where most of the wave's lanes take part, rather than in a sparser traversal step
 #pragma unroll
                 for (int k = 0; k < (!ft_none(F) && (F & FT_LINL) ? JT_FIRST_POP : JT_FIRST_POP_NONE); k++)
                     if (wants_node<WIDE>(T)) node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, oslot, cnt);
             }
         }
+#if JT_STAMPS
+        const unsigned long long ts5 = __builtin_amdgcn_s_memtime();
+        t_shade += ts5 - ts2;
+        t_hit += ts3 - ts2;
+        t_fin += ts4 - ts3;
+        t_qb += ts5 - ts4;
+#endif
         if (WC) {
             w_paths += lane_count(__builtin_amdgcn_ballot_w64(c_path));
             w_lq += lane_count(__builtin_amdgcn_ballot_w64(c_lq));
             w_rays += lane_count(__builtin_amdgcn_ballot_w64(c_ray));
             if (SAMPLER == 1 && chains_inline(F, S)) w_lq += __builtin_amdgcn_readfirstlane(wave_sum(n_inl));
         }
-        // publish the completed chunks: the wave's write-through stores drained, then each
-        // completing lane's done word (chunks accumulated of its pixel in this launch)
-        if (__builtin_amdgcn_ballot_w64(c_done)) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (c_done) {
-                __hip_atomic_store(A.tile_done + (item & ITEM_SLOT_MASK), item_chunk(item) + 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                item = ITEM_NONE;
-            }
-        }
     }
+#if JT_STAMPS
+    if (lane == 0) {
+        unsigned long long* dbg = A.counters + 8;
+        const unsigned long long v[24] = {t_trav, t_shade, n_trav,  n_shade, lanes_p, lanes_n,  steps_p, steps_n,
+                                          0,      t_hit,   t_fin,   t_qb,    0,       n_phit,   n_fin,   idle,
+                                          n_mph,  n_mty,   n_mid,   lanes_sh, lanes_hit, t_start, n_start, lanes_start};
+        for (int k = 0; k < 24; k++) atomicAdd(dbg + k, v[k]);
+    }
+#endif
+    // one atomic per counter per wave (the wave's own LDS adds precede this read in program order)
     const unsigned wv[3] = {w_paths, w_rays, w_lq};
     unsigned v[7] = {0u, 0u, 0u, cnt.nodes, cnt.instances, cnt.prims, COUNT ? cnt.shades : 0u};
 #pragma unroll
@@ -2099,6 +1773,13 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
     }
 }
 
+// The launch's last step when k > 1 (combine_kernel, jt_trace.hip): each pixel's stream means
+// combined in stream order, mean = sum_j mean_j * w_j over the streams with samples (w_j = n_j /
+// n, host-computed in double and rounded once), hits = sum_j hits_j.
+struct DCombine {
+    float w[JT_MAX_STREAMS];
+    int ns;  // streams with samples: min(k, n)
+};
 // Occupancy request (waves per SIMD); JT_WAVES=0 leaves it to the compiler. The LDS-mode
 // FT_NONE kernel (cornellbox: 96 VGPRs, LDS for 5 workgroups per CU with the stack sized to the
 // scene) asks for JT_WAVES_NONE: measured +4 % over 4 waves with its wait_lanes of 56.
@@ -2150,10 +1831,7 @@ __device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob)
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool WIDE>
 __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU void trace_kernel(DScene S, DParams P, int s_begin, int s_end, DAccum A) {
     __shared__ int lds_stack[RING * BLOCK];
-    if constexpr (JT_LANE_ITEMS && !JT_STAMPS)
-        trace_body_items<SAMPLER, RING, OVF, COUNT, F, true, WIDE>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
-    else
-        trace_body<SAMPLER, RING, OVF, COUNT, F, true, WIDE>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
+    trace_body_items<SAMPLER, RING, OVF, COUNT, F, true, WIDE>(S, P, s_begin, s_end, A, lds_stack + threadIdx.x);
 }
 
 // LDS mode (small scenes): the workgroup stages the scene blob into LDS once; every node,
@@ -2167,10 +1845,7 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(D
     for (int k = threadIdx.x; k < S.blob_n16; k += BLOCK) blob[k] = S.blob[k];
     __syncthreads();
     const DScene L = blob_scene(S, blob);
-    if constexpr (JT_LANE_ITEMS && !JT_STAMPS)
-        trace_body_items<SAMPLER, RING, OVF, COUNT, F, false, WIDE>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
-    else
-        trace_body<SAMPLER, RING, OVF, COUNT, F, false, WIDE>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
+    trace_body_items<SAMPLER, RING, OVF, COUNT, F, false, WIDE>(L, P, s_begin, s_end, A, reinterpret_cast<int*>(dyn_lds) + threadIdx.x);
 }
 
 // Persistent launch: as many workgroups as the device holds at once (capped by the number of

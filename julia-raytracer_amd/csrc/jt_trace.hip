@@ -78,9 +78,7 @@ struct jt_ctx {
     int width = 0, height = 0;
     int total_samples = 0, batch = 1, sampler = 1;
     int cus = 256;   // compute units of the device (persistent grid size)
-    int chunk = 0;   // samples per work unit (0: chosen per launch)
-    int chunk_min = -1;  // > 0: the launch's chunk table ends with a halving tail down to this many
-                         // samples; 0: uniform chunks; -1: auto (LDS mode: half a chunk)
+    int lk = 0;      // log2 of the sample streams per pixel (DParams::lk; fixed at jt_create)
     int tiles = 0;   // 8x8 pixel tiles
     int stack = 16;  // stack bound of the scene (entries); > 16: LDS ring of `ring` + HBM overflow
     int ring = 16;
@@ -90,7 +88,8 @@ struct jt_ctx {
     int traversal = 0;   // jt_params.traversal as resolved (JT_TRAVERSAL_AUTO: near or wide)
     int first = -1, next = 0;  // running-mean origin and next expected sample
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
-    bool failed = false;       // a launch's tile-order wait timed out: the running means are unusable
+    bool failed = false;       // a launch failed: the running means are unusable
+    bool stale = true;         // the accumulators are not yet zeroed or overwritten since jt_reset
     bool env_alias = false;    // JT_ENV_ALIAS=1: environment lights sample through alias tables
                                // until jt_reset
     size_t lds_scene_bytes = 0;  // > 0: small-scene LDS mode
@@ -110,11 +109,45 @@ struct jt_ctx {
     long long* red_hits = nullptr;
 };
 
+namespace jtk {
+// the combine of every pixel's stream means (DCombine, jt_kernels.h), one thread per pixel of
+// the launch's tiles; stream j's records of neighbouring pixels are contiguous (coalesced)
+__global__ __launch_bounds__(256) void combine_kernel(DParams P, DAccum A, DCombine Cw) {
+    const int tiles_x = (P.width + 7) / 8, tiles = launch_tiles(P);
+    const int g = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (g >= tiles * 64) return;
+    const int t = (g >> 6) * P.tile_stride + P.tile_offset, l = g & 63;
+    const int i = (t % tiles_x) * 8 + (l & 7), j = (t / tiles_x) * 8 + (l >> 3);
+    if (i >= P.width || j >= P.height) return;
+    const size_t pixel = (size_t)j * P.width + i, np = (size_t)A.npix;
+    float4 im = A.part_img[pixel], al = A.part_alb[pixel], nr = A.part_nrm[pixel];
+    const float w0 = Cw.w[0];
+    long long h = __float_as_int(al.w);
+    im = make_float4(im.x * w0, im.y * w0, im.z * w0, im.w * w0);
+    al = make_float4(al.x * w0, al.y * w0, al.z * w0, 0.0f);
+    nr = make_float4(nr.x * w0, nr.y * w0, nr.z * w0, 0.0f);
+    for (int s = 1; s < Cw.ns; s++) {
+        const float w = Cw.w[s];
+        const float4 a = A.part_img[s * np + pixel], b = A.part_alb[s * np + pixel], c = A.part_nrm[s * np + pixel];
+        im = make_float4(im.x + a.x * w, im.y + a.y * w, im.z + a.z * w, im.w + a.w * w);
+        al = make_float4(al.x + b.x * w, al.y + b.y * w, al.z + b.z * w, 0.0f);
+        nr = make_float4(nr.x + c.x * w, nr.y + c.y * w, nr.z + c.z * w, 0.0f);
+        h += __float_as_int(b.w);
+    }
+    A.image[pixel] = im;
+    A.albedo[pixel] = al;
+    A.normal[pixel] = nr;
+    A.hits[pixel] = h;
+}
+
+}  // namespace jtk
+
 namespace {
 
 int hip_fail(hipError_t e, const char* what) {
     return jt::fail(JT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
+int zero_if_stale(jt_ctx* c);
 
 // RCCL, loaded on first use by a multi-device context (dlopen of the ROCm install's
 // librccl.so.1): single-device contexts never touch it, and a process that already loaded an
@@ -352,9 +385,20 @@ int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_wo
     return rec[0];
 }
 
-// the launch schedule: a unit counter per XCD band, then a done word per pixel slot (tile * 64 + l:
-// chunks accumulated in this launch; the tile-unit body uses one word per tile, the first tiles)
-size_t sched_bytes(int tiles) { return ((size_t)tiles * 64 + NBANDS * BAND_STRIDE) * 4; }
+// the launch schedule: a unit counter per XCD band
+constexpr size_t SCHED_BYTES = (size_t)NBANDS * BAND_STRIDE * 4;
+
+// Sample streams per pixel (DESIGN.md §2 "Sample streams"), fixed at jt_create: 1 for the
+// reference's default one-sample batches (its single running mean), else the largest power of
+// two <= min(batch, JT_MAX_STREAMS) that keeps (pixels traced) x streams <= JT_STREAM_ITEMS:
+// enough independent (pixel, stream) items to fill the device with a short tail even when a
+// context traces only a tile share of the image, and stream means of at most JT_STREAM_ITEMS x
+// 48 B. The option "streams" (a power of two <= JT_MAX_STREAMS) overrides.
+int stream_log2(long long pixels, int batch) {
+    int lk = 0;
+    while (lk < 6 && (2 << lk) <= batch && (2 << lk) <= JT_MAX_STREAMS && pixels * (2LL << lk) <= JT_STREAM_ITEMS) lk++;
+    return lk;
+}
 
 int check_tree(const jt_bvh_tree& t, int nprims_expected, const char* what) {
     if (t.nprimitives != nprims_expected) return jt::fail(JT_ERR_INVALID, std::string(what) + ": primitive count mismatch");
@@ -1061,11 +1105,16 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             P.tile_offset = o;
         }
     }
-    // lanes that must be waiting before a shading phase runs; tunable
-    P.chunk = 0;  // 0: per launch, a quarter of its samples within [8, 64] (enough units per wave)
-    if (const char* ch = opt("chunk")) P.chunk = std::max(1, std::atoi(ch));
-    c->chunk = P.chunk;
-    if (const char* cm = opt("chunk_min")) c->chunk_min = std::max(0, std::atoi(cm));
+    // sample streams: from the pixels this context traces (a tile share traces 1/stride of them)
+    c->lk = stream_log2(((long long)W * H + P.tile_stride - 1) / P.tile_stride, std::max(1, params->batch));
+    if (const char* ks = opt("streams")) {
+        const int k = std::atoi(ks);
+        if (k < 1 || k > JT_MAX_STREAMS || (k & (k - 1)) != 0)
+            return bail(jt::fail(JT_ERR_INVALID, "option streams: a power of two in [1, " + std::to_string(JT_MAX_STREAMS) + "]"));
+        c->lk = 0;
+        while ((1 << c->lk) < k) c->lk++;
+    }
+    P.lk = c->lk;
     // measured best (cornellbox): 40 waiting lanes per shading phase; 48 with
     // light-hit steps in the traversal phase (they take the light queries out of the phases)
     bool inst_light = false;  // sample_lights_pdf runs instance queries (light-hit steps can run)
@@ -1099,18 +1148,26 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     c->allocations.push_back(hits);
     if ((e = hipMalloc(&cnt, 32 * 8)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc counters"));
     c->allocations.push_back(cnt);
-    // persistent scheduling: unit counters + per-pixel chunk counters (zeroed before each launch)
+    // persistent scheduling: unit counters (zeroed before each launch)
     c->tiles = ((W + 7) / 8) * ((H + 7) / 8);
-    if (c->tiles >= (1 << 20))  // the per-lane work items address a pixel as tile * 64 + l in 26 bits
+    if (c->tiles >= (1 << 20))  // the per-lane work items address a pixel as tile * 64 + l
         return bail(jt::fail(JT_ERR_UNSUPPORTED, "image above 2^20 8x8 tiles (67 Mpixels)"));
     void* sched = nullptr;
-    if ((e = hipMalloc(&sched, sched_bytes(c->tiles))) != hipSuccess)
-        return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc schedule"));
+    if ((e = hipMalloc(&sched, SCHED_BYTES)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc schedule"));
     c->allocations.push_back(sched);
+    // the sample streams' means (k > 1): image, albedo + hits, normal per (stream, pixel)
+    void* part[3] = {nullptr, nullptr, nullptr};
+    if (c->lk > 0) {
+        for (int k = 0; k < 3; k++) {
+            if ((e = hipMalloc(&part[k], np * 16 << c->lk)) != hipSuccess)
+                return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc stream means"));
+            c->allocations.push_back(part[k]);
+        }
+    }
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, params->device) == hipSuccess && cus > 0) c->cus = cus;
-    c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt,
-                  (unsigned*)sched, (int*)sched + NBANDS * BAND_STRIDE};
+    c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt, (unsigned*)sched,
+                  (float4*)part[0], (float4*)part[1], (float4*)part[2], (int)np};
     st = jt_reset(c);
     if (st != JT_OK) return bail(st);
     *out = c;
@@ -1160,6 +1217,12 @@ int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lig
     for (int d = 0; d < ndevices; d++) {
         c->sub[d]->P.tile_stride = c->tile_split ? ndevices : 1;
         c->sub[d]->P.tile_offset = c->tile_split ? d : 0;
+        // a device's share leaves the other devices' tiles at zero for the summing reduce
+        const int st = c->tile_split ? zero_if_stale(c->sub[d]) : JT_OK;
+        if (st != JT_OK) {
+            jt_destroy(c);
+            return st;
+        }
     }
     c->comms.resize(ndevices);
     ncclResult_t r = rccl().CommInitAll(c->comms.data(), ndevices, devs.data());
@@ -1185,6 +1248,23 @@ int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lig
     return JT_OK;
 }
 
+namespace {
+int zero_if_stale(jt_ctx* c) {
+    if (!c->stale) return JT_OK;
+    (void)hipSetDevice(c->device);
+    const size_t np = (size_t)c->width * (size_t)c->height;
+    hipError_t e;
+    if ((e = hipMemsetAsync(c->A.image, 0, np * 16, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->A.albedo, 0, np * 16, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->A.normal, 0, np * 16, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->A.hits, 0, np * 8, c->stream)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync");
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    c->stale = false;
+    return JT_OK;
+}
+}  // namespace
+
 int jt_reset(jt_ctx* c) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
     if (!c->sub.empty()) {
@@ -1201,14 +1281,17 @@ int jt_reset(jt_ctx* c) {
         return JT_OK;
     }
     (void)hipSetDevice(c->device);
-    const size_t np = (size_t)c->width * (size_t)c->height;
     hipError_t e;
-    if ((e = hipMemsetAsync(c->A.image, 0, np * 16, c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->A.albedo, 0, np * 16, c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->A.normal, 0, np * 16, c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->A.hits, 0, np * 8, c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->A.counters, 0, 256, c->stream)) != hipSuccess)
-        return hip_fail(e, "hipMemsetAsync");
+    if ((e = hipMemsetAsync(c->A.counters, 0, 256, c->stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    // make_trace_state's zeroed buffers (src/trace.jl:189-213). A context that traces every tile
+    // overwrites every pixel in its first launch without reading it (a stream's first sample
+    // starts from zero), so they are zeroed only if read before that launch (zero_if_stale); a
+    // tile share keeps the other tiles' pixels at zero for the reduce, so it zeroes them now.
+    c->stale = true;
+    if (c->P.tile_stride != 1) {
+        const int st = zero_if_stale(c);
+        if (st != JT_OK) return st;
+    }
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     c->first = -1;
     c->next = 0;
@@ -1221,50 +1304,14 @@ int jt_reset(jt_ctx* c) {
 }  // extern "C"
 
 namespace {
-// enqueue one launch over global samples [s0, s1) whose running-mean weight is 1/(s - first + 1)
+// enqueue one launch over global samples [s0, s1) of a context whose local samples start at
+// `first` (stream t & (k-1) of local sample t = s - first, DParams::lk), then — with k > 1 — the
+// combine of every pixel's stream means into the image and AOV buffers
 int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
     c->P.first = first;
-    // Samples per work unit: a sixteenth of the launch (JT_CHUNKS_PER_LAUNCH). Under the per-lane
-    // work items a lane done with its pixel's chunk takes the next pixel at once, so short units
-    // cost no wave-level tail, and the launch ends on short units: measured against the round-3
-    // rule (LDS mode a quarter of the launch within [8, 64]; HBM mode >= 32 units per resident
-    // wave, up to 256 samples), cornellbox 256 spp +3.0 % (chunk 64 -> 16), its 1/2, 1/4, 1/8
-    // sample shares +3.7 %, +5 %, +5.4 % (128, 64, 32 spp: chunk 8, 4, 2), bathroom1 128 spp
-    // +1.3 %, features2 128 spp +0.4 %, ecosys 16 spp +5.7 % (gpurun_out/r04h/chunk,
-    // r04i/chunk). Results do not depend on the chunking.
-    const int nsamp = s1 - s0;
-    if (c->chunk > 0) {
-        c->P.chunk = c->chunk;
-    } else {
-        c->P.chunk = std::max(1, (nsamp + JT_CHUNKS_PER_LAUNCH - 1) / JT_CHUNKS_PER_LAUNCH);
-    }
-    // chunk table with a halving tail: full chunks while more than two remain, then halves down
-    // to chunk_min samples, so the launch ends on short units (results do not depend on chunking)
-    // Auto: LDS-mode (small-scene) launches of >= 32-sample chunks end on half chunks: +1.2 % on
-    // cornellbox 256 spp, +0.7 % at 128 spp (32 spp: within noise); HBM-mode scenes gain nothing
-    // (bathroom1 even, features2 -2 %)
-    // (profiles/r02_chunk_tail.txt)
-    const int cmin = c->chunk_min >= 0 ? c->chunk_min : (c->lds_scene_bytes > 0 && c->P.chunk >= 32 ? c->P.chunk / 2 : 0);
-    c->P.nct = 0;
-    // at most JT_MAX_CHUNKS chunks per launch (the per-lane work items keep a pixel's chunk in 5 bits)
-    if ((nsamp + c->P.chunk - 1) / c->P.chunk > JT_MAX_CHUNKS) c->P.chunk = (nsamp + JT_MAX_CHUNKS - 1) / JT_MAX_CHUNKS;
-    if (cmin > 0 && cmin < c->P.chunk) {
-        int rem = s1 - s0, n = 0, at = 0;
-        c->P.cbeg[0] = 0;
-        while (rem > 0 && n < JT_MAX_CHUNKS) {
-            int k = rem > 2 * c->P.chunk ? c->P.chunk : std::max(cmin, (rem + 1) / 2);
-            k = std::min(k, rem);
-            at += k;
-            rem -= k;
-            c->P.cbeg[++n] = at;
-        }
-        if (rem == 0) c->P.nct = n;
-    }
     (void)hipSetDevice(c->device);
-    hipError_t e = hipMemsetAsync(c->A.work, 0, sched_bytes(c->tiles), c->stream);
+    hipError_t e = hipMemsetAsync(c->A.work, 0, SCHED_BYTES, c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
-    // counter [7] counts this launch's tile-order wait timeouts only
-    if ((e = hipMemsetAsync(c->A.counters + 7, 0, 8, c->stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if (c->sampler == JT_SAMPLER_NAIVE)
         e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
@@ -1273,7 +1320,20 @@ int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
         e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
                      : launch_s<1, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
+    if (c->lk > 0) {
+        // weights n_j / n of the streams after this launch: n local samples, stream j holds
+        // those t < n with t mod k == j (include/jtrace.h jt_get_streams restates the rule)
+        const long long n = (long long)s1 - first, k = 1LL << c->lk;
+        DCombine cw{};
+        cw.ns = (int)std::min(n, k);
+        for (int j = 0; j < cw.ns; j++) cw.w[j] = (float)((double)((n - 1 - j) / k + 1) / (double)n);
+        const int tiles = launch_tiles(c->P);
+        const int nblk = (int)(((long long)tiles * 64 + 255) / 256);
+        if (nblk > 0) hipLaunchKernelGGL(combine_kernel, dim3(nblk), dim3(256), 0, c->stream, c->P, c->A, cw);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "combine kernel launch");
+    }
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    c->stale = false;  // every pixel of the launch's tiles was written (tile shares were zeroed at reset)
     return JT_OK;
 }
 // wait for the launch; its device time in *ms
@@ -1285,12 +1345,6 @@ int trace_finish(jt_ctx* c, float* ms) {
     (void)hipEventElapsedTime(ms, c->ev0, c->ev1);
     c->kernel_ms += *ms;
     c->launches++;
-    unsigned long long timeouts = 0;
-    if ((e = hipMemcpy(&timeouts, c->A.counters + 7, 8, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "hipMemcpy");
-    if (timeouts) {  // a wave accumulated without its predecessor chunk: the means are corrupt
-        c->failed = true;
-        return jt::fail(JT_ERR_DEVICE, "work-unit ordering wait timed out");
-    }
     return JT_OK;
 }
 
@@ -1404,10 +1458,12 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     if (c->first < 0) c->first = s0;
     if (!c->sub.empty()) return multi_trace_range(c, s0, s1);
     int st = trace_launch(c, s0, s1, c->first);
-    if (st != JT_OK) return st;
     float ms = 0;
-    st = trace_finish(c, &ms);
-    if (st != JT_OK) return st;
+    if (st == JT_OK) st = trace_finish(c, &ms);
+    if (st != JT_OK) {
+        c->failed = true;
+        return st;
+    }
     c->next = s1;
     return JT_OK;
 }
@@ -1418,6 +1474,12 @@ int jt_trace_samples(jt_ctx* c) {
     if (n >= c->total_samples) return JT_OK;  // state.samples >= params.samples
     const int target = std::min(n + c->batch, c->total_samples);
     return jt_trace_range(c, n, target);
+}
+
+int jt_get_streams(const jt_ctx* c, int32_t* streams) {
+    if (!c || !streams) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    *streams = 1 << (c->sub.empty() ? c->lk : c->sub[0]->lk);
+    return JT_OK;
 }
 
 int jt_get_samples(const jt_ctx* c, int32_t* samples) {
@@ -1436,7 +1498,12 @@ int jt_get_size(const jt_ctx* c, int32_t* w, int32_t* h) {
 int jt_get_image(jt_ctx* c, float* rgba) {
     if (!c || !rgba) return jt::fail(JT_ERR_INVALID, "NULL argument");
     if (c->failed) return jt::fail(JT_ERR_STATE, "the running means are corrupt (a launch failed); jt_reset the context");
-    if (!c->sub.empty()) return multi_reduce(c, 0, rgba, nullptr);
+    if (!c->sub.empty()) {
+        for (jt_ctx* s : c->sub)
+            if (const int st = zero_if_stale(s)) return st;
+        return multi_reduce(c, 0, rgba, nullptr);
+    }
+    if (const int st = zero_if_stale(c)) return st;
     (void)hipSetDevice(c->device);
     hipError_t e = hipMemcpy(rgba, c->A.image, (size_t)c->width * c->height * 16, hipMemcpyDeviceToHost);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy image");
@@ -1445,6 +1512,10 @@ int jt_get_image(jt_ctx* c, float* rgba) {
 int jt_get_aovs(jt_ctx* c, float* albedo, float* normal, int64_t* hits) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
     if (c->failed) return jt::fail(JT_ERR_STATE, "the running means are corrupt (a launch failed); jt_reset the context");
+    for (jt_ctx* s : c->sub)
+        if (const int st = zero_if_stale(s)) return st;
+    if (c->sub.empty())
+        if (const int st = zero_if_stale(c)) return st;
     (void)hipSetDevice(c->device);
     const size_t np = (size_t)c->width * c->height;
     std::vector<float4> tmp(np);
@@ -1525,6 +1596,7 @@ int jt_get_counters(jt_ctx* c, jt_counters* out) {
 int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
     if (!c || !out) return jt::fail(JT_ERR_INVALID, "NULL argument");
     if (!c->sub.empty()) return jt_get_device_buffers(c->sub[0], out);  // device 0's share
+    if (const int st = zero_if_stale(c)) return st;
     out->image = c->A.image;
     out->albedo = c->A.albedo;
     out->normal = c->A.normal;
@@ -1536,10 +1608,10 @@ int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
 }
 
 // diagnostic build only (JT_STAMPS=1): per-phase wave clocks and shading-phase material coherence
-// (19 u64), read by scripts/stamps.py
+// (24 u64), read by scripts/stamps.py
 extern "C" int jt_debug_stamps(jt_ctx* c, unsigned long long* out8) {
     if (!c || !out8) return jt::fail(JT_ERR_INVALID, "NULL argument");
-    hipError_t e = hipMemcpy(out8, c->A.counters + 8, 19 * 8, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpy(out8, c->A.counters + 8, 24 * 8, hipMemcpyDeviceToHost);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy stamps");
 }
 
@@ -1561,12 +1633,12 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
     char tmp[640];
     std::snprintf(tmp, sizeof tmp,
                   "kernel=%s<%d,%d,%s,%d,%d,%s> mode=%s scene_lds_bytes=%zu stack_bound=%d lds_ring=%d hbm_overflow=%d "
-                  "wait_lanes=%d light_lanes=%d chunk=%d chunk_table=%d tiles=%d block=%d env_alias=%d light_inline=%d "
+                  "wait_lanes=%d light_lanes=%d streams=%d tiles=%d block=%d env_alias=%d light_inline=%d "
                   "traversal=%s%s",
                   c->lds_scene_bytes ? "trace_kernel_lds" : "trace_kernel", c->sampler == JT_SAMPLER_NAIVE ? 2 : 1,
                   ring, ovf ? "true" : "false", c->count, c->kmask, c->wide ? "true" : "false",
                   c->lds_scene_bytes ? "lds" : "hbm", c->lds_scene_bytes,
-                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, c->P.chunk, c->P.nct, c->tiles, BLOCK,
+                  c->stack, ring, ovf ? 1 : 0, c->P.wait_lanes, c->P.light_lanes, 1 << c->lk, c->tiles, BLOCK,
                   c->env_alias ? 1 : 0, c->S.light_inline,
                   c->traversal == JT_TRAVERSAL_REFERENCE ? "reference" : c->traversal == JT_TRAVERSAL_NEAR ? "near" : "wide",
                   filt);

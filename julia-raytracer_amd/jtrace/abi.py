@@ -269,6 +269,7 @@ def _declare(lib):
     lib.jt_trace_samples.argtypes = [C.c_void_p]
     lib.jt_trace_range.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
     lib.jt_get_samples.argtypes = [C.c_void_p, i32p]
+    lib.jt_get_streams.argtypes = [C.c_void_p, i32p]
     lib.jt_get_size.argtypes = [C.c_void_p, i32p, i32p]
     lib.jt_get_image.argtypes = [C.c_void_p, f32p]
     lib.jt_get_aovs.argtypes = [C.c_void_p, f32p, f32p, C.POINTER(C.c_int64)]
@@ -287,7 +288,7 @@ def _declare(lib):
 EXPORTED_SYMBOLS = [
     "jt_version", "jt_abi_version", "jt_last_error", "jt_device_count", "jt_set_option", "jt_build_scene_bvh",
     "jt_free_scene_bvh", "jt_make_lights", "jt_free_lights", "jt_image_size", "jt_create", "jt_create_multi",
-    "jt_trace_samples", "jt_trace_range", "jt_get_samples", "jt_get_size", "jt_get_image",
+    "jt_trace_samples", "jt_trace_range", "jt_get_streams", "jt_get_samples", "jt_get_size", "jt_get_image",
     "jt_get_aovs", "jt_get_counters", "jt_reset", "jt_get_device_buffers", "jt_set_counters", "jt_describe", "jt_synchronize",
     "jt_destroy",
 ]

@@ -120,6 +120,14 @@ class TraceState:
         abi.check(self.lib, self.lib.jt_get_samples(self.handle, C.byref(n)))
         return n.value
 
+    @property
+    def streams(self) -> int:
+        """Sample streams per pixel k (jt_get_streams): local sample t goes to stream t mod k, and
+        the image is the streams' running means combined in stream order (include/jtrace.h)."""
+        n = C.c_int32()
+        abi.check(self.lib, self.lib.jt_get_streams(self.handle, C.byref(n)))
+        return n.value
+
     def get_image(self) -> np.ndarray:
         out = np.empty((self.height, self.width, 4), np.float32)
         abi.check(self.lib, self.lib.jt_get_image(self.handle, out.ctypes.data_as(abi.f32p)))

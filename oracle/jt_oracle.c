@@ -1746,18 +1746,27 @@ static ray3 sample_camera(const ctx_t* c, const jt_camera* cam, int i, int j, v2
 
 typedef struct {
     const ctx_t* c;
-    int32_t first, s0, s1, row0, row1, nthreads, tid;
+    int32_t first, s0, s1, row0, row1, nthreads, tid, lk;
     float *image, *albedo, *normal;
     int64_t* hits;
+    /* the sample streams' running means (lk > 0): stream j of pixel p at [j * W*H + p] */
+    float *part_img, *part_alb, *part_nrm;
+    int64_t* part_hits;
     scratch_t sc;
 } worker_t;
 
-/* trace_sample (src/trace.jl:584-649) for one pixel over [s0, s1) */
+/* trace_sample (src/trace.jl:584-649) for one pixel over [s0, s1).
+ * Sample streams (the build's accumulation contract, include/jtrace.h jt_trace_range): local
+ * sample t = sample - first belongs to stream t mod 2^lk and is its (t >> lk)-th sample; each
+ * stream keeps the reference's running mean of its own samples (src/trace.jl:631-648). lk = 0 is
+ * the reference's single running mean over all samples, kept in the image buffers themselves.
+ * After the range the streams are combined into the image buffers (combine_pixel). */
 static void trace_pixel(worker_t* w, int i, int j) {
     const ctx_t* c = w->c;
     const jt_params* params = c->params;
     const jt_camera* cam = &c->scene->cameras[params->camera];
     long idx = (long)c->width * j + i;
+    const long npix = (long)c->width * c->height;
     for (int32_t sample = w->s0; sample < w->s1; sample++) {
         rng_t rng = rng_init(params->seed, (int32_t)idx, sample);
         v2 puv = rand2f(&rng);
@@ -1771,10 +1780,13 @@ static void trace_pixel(worker_t* w, int i, int j) {
         if (!isfinite3(radiance)) radiance = V3(0, 0, 0);
         float mr = max3f(radiance);
         if (mr > (float)params->clamp) radiance = scl3(radiance, (float)params->clamp / mr);
-        float weight = 1.0f / (float)(sample - w->first + 1);
-        float* im = &w->image[4 * idx];
-        float* al = &w->albedo[3 * idx];
-        float* nm = &w->normal[3 * idx];
+        const int32_t t = sample - w->first;
+        const long sidx = w->lk ? (long)(t & ((1 << w->lk) - 1)) * npix + idx : idx;
+        float weight = 1.0f / (float)((t >> w->lk) + 1);
+        float* im = w->lk ? &w->part_img[4 * sidx] : &w->image[4 * idx];
+        float* al = w->lk ? &w->part_alb[3 * sidx] : &w->albedo[3 * idx];
+        float* nm = w->lk ? &w->part_nrm[3 * sidx] : &w->normal[3 * idx];
+        int64_t* hp = w->lk ? &w->part_hits[sidx] : &w->hits[idx];
         v4 img = V4(im[0], im[1], im[2], im[3]);
         v3 alb = V3(al[0], al[1], al[2]);
         v3 nrm = V3(nm[0], nm[1], nm[2]);
@@ -1784,12 +1796,12 @@ static void trace_pixel(worker_t* w, int i, int j) {
             target4 = V4(radiance.x, radiance.y, radiance.z, 1);
             target_a = r.albedo;
             target_n = r.normal;
-            w->hits[idx] += 1;
+            *hp += 1;
         } else if (!params->envhidden && c->scene->nenvironments != 0) {
             target4 = V4(radiance.x, radiance.y, radiance.z, 1);
             target_a = V3(1, 1, 1);
             target_n = neg3(ray.d);
-            w->hits[idx] += 1;
+            *hp += 1;
         } else {
             target4 = V4(0, 0, 0, 0);
             target_a = V3(0, 0, 0);
@@ -1807,12 +1819,36 @@ static void trace_pixel(worker_t* w, int i, int j) {
     }
 }
 
+/* the streams' means combined in stream order after the range (include/jtrace.h jt_trace_range):
+ * n local samples so far, stream j holds n_j of them, w_j = (float)((double)n_j / n);
+ * mean = mean_0 * w_0 + mean_1 * w_1 + ... (no FMA), hits = sum_j hits_j */
+static void combine_pixel(worker_t* w, long idx) {
+    const long npix = (long)w->c->width * w->c->height;
+    const long n = (long)w->s1 - w->first, k = 1L << w->lk;
+    const long ns = n < k ? n : k;
+    float im[4] = {0, 0, 0, 0}, al[3] = {0, 0, 0}, nm[3] = {0, 0, 0};
+    int64_t h = 0;
+    for (long s = 0; s < ns; s++) {
+        const float ws = (float)((double)((n - 1 - s) / k + 1) / (double)n);
+        const long o = s * npix + idx;
+        for (int q = 0; q < 4; q++) im[q] = s == 0 ? w->part_img[4 * o + q] * ws : im[q] + w->part_img[4 * o + q] * ws;
+        for (int q = 0; q < 3; q++) al[q] = s == 0 ? w->part_alb[3 * o + q] * ws : al[q] + w->part_alb[3 * o + q] * ws;
+        for (int q = 0; q < 3; q++) nm[q] = s == 0 ? w->part_nrm[3 * o + q] * ws : nm[q] + w->part_nrm[3 * o + q] * ws;
+        h += w->part_hits[o];
+    }
+    for (int q = 0; q < 4; q++) w->image[4 * idx + q] = im[q];
+    for (int q = 0; q < 3; q++) w->albedo[3 * idx + q] = al[q];
+    for (int q = 0; q < 3; q++) w->normal[3 * idx + q] = nm[q];
+    w->hits[idx] = h;
+}
+
 static void* worker_main(void* arg) {
     worker_t* w = (worker_t*)arg;
     for (int j = w->row0 + w->tid; j < w->row1; j += w->nthreads) {
         for (int i = 0; i < w->c->width; i++) {
             trace_pixel(w, i, j);
             if (w->sc.overflow) return NULL;
+            if (w->lk) combine_pixel(w, (long)w->c->width * j + i);
         }
     }
     return NULL;
@@ -1872,8 +1908,10 @@ static void free_ctx(ctx_t* c) {
 
 int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights, const jt_params* params,
                   int32_t width, int32_t height, int32_t row0, int32_t row1, int32_t first, int32_t s0, int32_t s1,
-                  float* image, float* albedo, float* normal, int64_t* hits, int32_t nthreads, or_counters* counters) {
+                  float* image, float* albedo, float* normal, int64_t* hits, int32_t lk, float* part_img,
+                  float* part_alb, float* part_nrm, int64_t* part_hits, int32_t nthreads, or_counters* counters) {
     if (!scene || !bvh || !lights || !params || !image || !albedo || !normal || !hits) return JT_ERR_INVALID;
+    if (lk < 0 || lk > 6 || (lk > 0 && (!part_img || !part_alb || !part_nrm || !part_hits))) return JT_ERR_INVALID;
     if (width <= 0 || height <= 0 || s0 < first || s1 < s0 || row0 < 0 || row1 > height) return JT_ERR_INVALID;
     if (nthreads < 1) nthreads = 1;
     ctx_t c;
@@ -1896,6 +1934,11 @@ int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_light
         w->albedo = albedo;
         w->normal = normal;
         w->hits = hits;
+        w->lk = lk;
+        w->part_img = part_img;
+        w->part_alb = part_alb;
+        w->part_nrm = part_nrm;
+        w->part_hits = part_hits;
         w->sc.stack = (int32_t*)malloc(sizeof(int32_t) * (size_t)ssize);
         w->sc.sub_stack = (int32_t*)malloc(sizeof(int32_t) * (size_t)ssize);
         w->sc.stack_size = ssize;
@@ -1932,7 +1975,7 @@ int or_trace(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* li
              int32_t width, int32_t height, int32_t first, int32_t s0, int32_t s1, float* image, float* albedo,
              float* normal, int64_t* hits, int32_t nthreads, or_counters* counters) {
     return or_trace_rows(scene, bvh, lights, params, width, height, 0, height, first, s0, s1, image, albedo, normal,
-                         hits, nthreads, counters);
+                         hits, 0, NULL, NULL, NULL, NULL, nthreads, counters);
 }
 
 /* ================================================================ BVH build (src/bvh.jl) */

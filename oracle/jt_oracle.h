@@ -32,19 +32,23 @@ void or_free_scene_bvh(jt_scene_bvh* bvh);
 int or_make_lights(const jt_scene* scene, jt_lights* out);
 void or_free_lights(jt_lights* lights);
 
-/* trace_samples (src/trace.jl:215-274) over global samples [s0, s1) for all W*H pixels,
- * running-mean weight 1/(s - first + 1). image: W*H*4, albedo/normal: W*H*3, hits: W*H.
- * Rows are split over nthreads pthreads. Returns 0 or a negative jt_status. */
+/* trace_samples (src/trace.jl:215-274) over global samples [s0, s1) for all W*H pixels into
+ * one running mean (one sample stream), weight 1/(s - first + 1). image: W*H*4, albedo/normal:
+ * W*H*3, hits: W*H. Rows are split over nthreads pthreads. Returns 0 or a negative jt_status. */
 int or_trace(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
              const jt_params* params, int32_t width, int32_t height, int32_t first,
              int32_t s0, int32_t s1, float* image, float* albedo, float* normal,
              int64_t* hits, int32_t nthreads, or_counters* counters);
 
-/* Row-restricted variant: pixels of rows [row0, row1) only (bounded CPU samples). */
+/* Row-restricted variant: pixels of rows [row0, row1) only (bounded CPU samples), with 2^lk
+ * sample streams (include/jtrace.h jt_trace_range): for lk > 0 the streams' running means live
+ * in part_img (k*W*H*4), part_alb / part_nrm (k*W*H*3) and part_hits (k*W*H), stream-major, and
+ * the rows' image / AOVs / hits are their combination after the range. */
 int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
                   const jt_params* params, int32_t width, int32_t height, int32_t row0,
                   int32_t row1, int32_t first, int32_t s0, int32_t s1, float* image,
-                  float* albedo, float* normal, int64_t* hits, int32_t nthreads,
+                  float* albedo, float* normal, int64_t* hits, int32_t lk, float* part_img,
+                  float* part_alb, float* part_nrm, int64_t* part_hits, int32_t nthreads,
                   or_counters* counters);
 
 /* Single-function known-answer entry points (tests/test_oracle_kat.py). */

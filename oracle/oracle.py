@@ -34,7 +34,7 @@ def _load(abi):
     lib.or_trace_rows.argtypes = [C.POINTER(abi.jt_scene), C.POINTER(abi.jt_scene_bvh), C.POINTER(abi.jt_lights),
                                   C.POINTER(abi.jt_params), C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                   C.c_int32, C.c_int32, C.c_int32, f32p, f32p, f32p, i64p, C.c_int32,
-                                  C.POINTER(Counters)]
+                                  f32p, f32p, f32p, i64p, C.c_int32, C.POINTER(Counters)]
     lib.or_intersect_triangle.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p, f32p, f32p]
     lib.or_intersect_bbox.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p]
     lib.or_fresnel_dielectric.argtypes = [C.c_float, f32p, f32p]
@@ -89,11 +89,20 @@ class Oracle:
         return {"records": out[0], "violations": out[1], "leaves": out[2], "volume_ratio": out[3] / 1000.0}
 
     def trace(self, scene_abi, bvh, lights, params, width, height, s0, s1, first=0, rows=None,
-              nthreads=None, state=None):
-        """Returns (image (H,W,4), albedo (H,W,3), normal (H,W,3), hits (H,W), counters)."""
+              nthreads=None, state=None, streams=1, parts=None):
+        """Returns (image (H,W,4), albedo (H,W,3), normal (H,W,3), hits (H,W), counters).
+
+        streams: the sample streams per pixel k (a power of two, the library's jt_get_streams;
+        include/jtrace.h jt_trace_range states the contract). For k > 1 the streams' running
+        means are kept in `parts` (a dict of arrays, created when None and filled in place), which
+        a caller passes again to continue the same render with a later range."""
         if params.traversal not in (0, 1, 2):
             raise ValueError(f"the oracle restates an explicit BVH order (0 reference, 1 near, 2 wide), got "
                              f"{params.traversal}: resolve auto (3) to the order the library ran first")
+        k = int(streams)
+        if k < 1 or k > 64 or k & (k - 1):
+            raise ValueError(f"streams must be a power of two in [1, 64], got {streams}")
+        lk = k.bit_length() - 1
         if nthreads is None:
             nthreads = min(16, os.cpu_count() or 1)
         if state is None:
@@ -103,13 +112,26 @@ class Oracle:
             hits = np.zeros((height, width), np.int64)
         else:
             image, albedo, normal, hits = state
+        f32p = C.POINTER(C.c_float)
+        i64p = C.POINTER(C.c_int64)
+        if lk > 0:
+            if parts is None:
+                parts = {}
+            if not parts:
+                parts.update(img=np.zeros((k, height, width, 4), np.float32),
+                             alb=np.zeros((k, height, width, 3), np.float32),
+                             nrm=np.zeros((k, height, width, 3), np.float32),
+                             hits=np.zeros((k, height, width), np.int64))
+            pp = (parts["img"].ctypes.data_as(f32p), parts["alb"].ctypes.data_as(f32p),
+                  parts["nrm"].ctypes.data_as(f32p), parts["hits"].ctypes.data_as(i64p))
+        else:
+            pp = (None, None, None, None)
         r0, r1 = rows if rows is not None else (0, height)
         cnt = Counters()
-        f32p = C.POINTER(C.c_float)
         st = self.lib.or_trace_rows(scene_abi.ref, C.byref(bvh.struct), C.byref(lights.struct), C.byref(params),
                                     width, height, r0, r1, first, s0, s1, image.ctypes.data_as(f32p),
                                     albedo.ctypes.data_as(f32p), normal.ctypes.data_as(f32p),
-                                    hits.ctypes.data_as(C.POINTER(C.c_int64)), nthreads, C.byref(cnt))
+                                    hits.ctypes.data_as(i64p), lk, *pp, nthreads, C.byref(cnt))
         if st != 0:
             raise RuntimeError(f"oracle trace failed: {st}")
         return image, albedo, normal, hits, cnt.as_dict()

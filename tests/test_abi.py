@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_version(lib):
-    assert lib.jt_abi_version() == 3  # 2: jt_params.traversal, 3: jt_set_option
+    assert lib.jt_abi_version() == 4  # 2: jt_params.traversal, 3: jt_set_option, 4: sample streams
     assert b"gfx950" in lib.jt_version()
 
 
@@ -65,7 +65,7 @@ def test_run_time_options_are_explicit(abi, lib):
     and clear, and the library never reads the environment (no getenv in the sources)."""
     assert lib.jt_set_option(b"no_such_option", b"1") == -1
     assert b"unknown option" in lib.jt_last_error()
-    for name in ("env_alias", "features", "lds_scene", "lds_stack", "light_inline", "chunk", "chunk_min",
+    for name in ("env_alias", "features", "lds_scene", "lds_stack", "light_inline", "streams",
                  "wait_lanes", "light_lanes", "multi_split", "tile_share", "test_lds_ring"):
         assert lib.jt_set_option(name.encode(), b"1") == 0
         assert lib.jt_set_option(name.encode(), None) == 0

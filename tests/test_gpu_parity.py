@@ -30,10 +30,12 @@ def _render_both(abi, lib, oracle, scene_abi, params, s0, s1, batch_calls=False)
     gimg = st.get_image()
     galb, gnrm, ghits = st.get_aovs()
     gcnt = st.counters()
+    k = st.streams
     st.close()
     ob = oracle.build_bvh(scene_abi)
     ol = oracle.make_lights(scene_abi)
-    oimg, oalb, onrm, ohits, ocnt = oracle.trace(scene_abi, ob, ol, params, gimg.shape[1], gimg.shape[0], s0, s1)
+    oimg, oalb, onrm, ohits, ocnt = oracle.trace(scene_abi, ob, ol, params, gimg.shape[1], gimg.shape[0], s0, s1,
+                                                 streams=k)
     return (gimg, galb, gnrm, ghits, gcnt), (oimg, oalb, onrm, ohits, ocnt)
 
 
@@ -55,21 +57,48 @@ def test_cornellbox_parity(gpu, abi, lib, oracle, cornell_abi, sampler):
 
 
 def test_batching_is_bitwise_invariant(gpu, abi, lib, cornell_abi):
-    """trace_samples with batch=1 called N times == one launch over [0, N) (running mean order)."""
+    """A render split into calls gives the bits of one call over the whole range, at one sample
+    stream (trace_samples with the reference's --batch 1, 6 calls) and at k streams (any split of
+    the range: every stream sees its samples in order, the image is their combination)."""
     from jtrace import trace
     bvh = trace.make_scene_bvh(cornell_abi, False, lib)
     lights = trace.make_trace_lights(cornell_abi, lib)
     p1 = make_params(abi, resolution=64, samples=6, batch=1)
     a = trace.make_trace_state(cornell_abi, bvh, lights, p1, lib)
+    assert a.streams == 1
     for _ in range(6):
         a.trace_samples()
     assert a.samples == 6
-    p2 = make_params(abi, resolution=64, samples=6, batch=6)
-    b = trace.make_trace_state(cornell_abi, bvh, lights, p2, lib)
-    b.trace_samples()
-    assert np.array_equal(a.get_image(), b.get_image())
+    one = trace.make_trace_state(cornell_abi, bvh, lights, p1, lib)
+    one.trace_range(0, 6)
+    assert np.array_equal(a.get_image(), one.get_image())
     a.trace_samples()  # state.samples >= params.samples: no-op, as the reference
     assert a.samples == 6
+    p2 = make_params(abi, resolution=64, samples=11, batch=11)
+    full = trace.make_trace_state(cornell_abi, bvh, lights, p2, lib)
+    assert full.streams == 8, full.describe()
+    full.trace_range(0, 11)
+    ref = (full.get_image(), full.get_aovs())
+    for cuts in ((0, 1, 11), (0, 3, 4, 10, 11), (0, 8, 11)):
+        b = trace.make_trace_state(cornell_abi, bvh, lights, p2, lib)
+        for s0, s1 in zip(cuts[:-1], cuts[1:]):
+            b.trace_range(s0, s1)
+        assert np.array_equal(b.get_image(), ref[0]), cuts
+        for x, y in zip(b.get_aovs(), ref[1]):
+            assert np.array_equal(x, y), cuts
+        b.close()
+    # one stream vs eight: the same samples, combined in another order (last bits only)
+    stats = compare_images(full.get_image(), trace_one(cornell_abi, bvh, lights, make_params(abi, resolution=64, samples=11, batch=1), lib))
+    assert stats["frac_pix_rel_le_1e-3"] >= 0.999 and stats["image_mean_rel"] <= 1e-5, stats
+
+
+def trace_one(sa, bvh, lights, p, lib):
+    from jtrace import trace
+    st = trace.make_trace_state(sa, bvh, lights, p, lib)
+    st.trace_range(0, p.samples)
+    img = st.get_image()
+    st.close()
+    return img
 
 
 def test_shard_combination_matches_single(gpu, abi, lib, cornell_abi):
@@ -194,34 +223,59 @@ def test_light_hit_steps_are_bitwise_invariant(gpu, abi, lib, cornell_abi, optio
 
 
 @pytest.mark.parametrize("sampler", [1, 2])
-def test_chunked_work_units_are_bitwise_invariant(gpu, abi, lib, cornell_abi, sampler, options):
-    """Work units = (sample chunk, 8x8 tile), fetched dynamically by waves: a tile's chunks are
-    accumulated in order (cross-XCD release/acquire), so any chunk size gives the same bits."""
+@pytest.mark.parametrize("k", ["2", "8", "64"])
+def test_sample_streams_match_the_oracle(gpu, abi, lib, oracle, cornell_abi, sampler, k, options):
+    """k sample streams per pixel (include/jtrace.h jt_trace_range), in two calls whose second
+    continues every stream's running mean from HBM, against the oracle's restatement of the same
+    streams and combination: at the parity bar, hits and paths exact."""
     from jtrace import trace
+    options("streams", k)
     bvh = trace.make_scene_bvh(cornell_abi, False, lib)
     lights = trace.make_trace_lights(cornell_abi, lib)
     p = make_params(abi, resolution=72, samples=9, sampler=sampler)
-    outs = []
-    # uniform chunks of 1000 (one per tile), 1 and 4 samples (option chunk_min=0); chunk tables
-    # ending in a halving tail: 4,3,1,1 and 2,2,2,2,1; the auto tail of 64-sample chunks (9 samples: one chunk)
-    for chunk, cmin in (("1000", "0"), ("1", "0"), ("4", "0"), ("4", "1"), ("2", "1"), ("64", None)):
-        options("chunk", chunk)
-        if cmin is None:
-            options("chunk_min", None)
-        else:
-            options("chunk_min", cmin)
-        st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
-        st.trace_range(0, 9)
-        outs.append((st.get_image(), st.get_aovs(), st.counters()))
-        desc = st.describe()
-        assert ("chunk_table=0" in desc) == (cmin == "0"), desc
+    st = trace.make_trace_state(cornell_abi, bvh, lights, p, lib)
+    assert st.streams == int(k) and f"streams={k}" in st.describe()
+    st.trace_range(0, 5)
+    st.trace_range(5, 9)
+    g = (st.get_image(), *st.get_aovs(), st.counters())
+    st.close()
+    ob, ol = oracle.build_bvh(cornell_abi), oracle.make_lights(cornell_abi)
+    parts = {}
+    oracle.trace(cornell_abi, ob, ol, p, 72, 72, 0, 5, streams=int(k), parts=parts)
+    o = oracle.trace(cornell_abi, ob, ol, p, 72, 72, 5, 9, streams=int(k), parts=parts,
+                     state=tuple(np.zeros(x.shape, x.dtype) for x in (g[0], g[1], g[2], g[3])))
+    stats = compare_images(g[0], o[0])
+    print("streams", k, "sampler", sampler, stats)
+    assert stats["frac_pix_rel_le_1e-3"] >= 0.999 and stats["image_mean_rel"] <= 1e-4, stats
+    assert stats["bitwise_frac"] >= 0.99, stats
+    assert np.array_equal(g[3], o[3])
+    for a, b in zip(g[1:3], o[1:3]):
+        assert compare_images(a, b)["frac_pix_rel_le_1e-3"] >= 0.999
+    assert g[4]["paths"] == 72 * 72 * 9
+
+
+def test_stream_count_rule(gpu, abi, lib, cornell_abi, options):
+    """jt_get_streams: 1 at --batch 1, else the largest power of two <= min(batch, 64) with
+    (pixels traced) x k <= 2^24 (include/jtrace.h); a tile share counts its own pixels."""
+    from jtrace import trace
+    bvh = trace.make_scene_bvh(cornell_abi, False, lib)
+    lights = trace.make_trace_lights(cornell_abi, lib)
+
+    def rule(px, batch):
+        k = 1
+        while 2 * k <= min(batch, 64) and px * 2 * k <= 1 << 24:
+            k *= 2
+        return k
+
+    for w, h, batch, share in ((1280, 720, 256, 1), (1280, 720, 1, 1), (256, 256, 16, 1), (1920, 1080, 1024, 1),
+                               (3840, 2160, 4096, 1), (1280, 720, 256, 8), (64, 64, 5, 1)):
+        options("tile_share", f"{share},0" if share > 1 else None)
+        st = trace.make_trace_state(cornell_abi, bvh, lights, make_params(abi, width=w, height=h, samples=batch,
+                                                                          batch=batch), lib)
+        tiles = ((w + 7) // 8) * ((h + 7) // 8)
+        px = w * h if share == 1 else -(-w * h // share)
+        assert st.streams == rule(px, batch), (w, h, batch, share, st.streams, tiles)
         st.close()
-    for o in outs[1:]:
-        assert np.array_equal(outs[0][0], o[0])
-        for a, b in zip(outs[0][1], o[1]):
-            assert np.array_equal(a, b)
-        for k in ("paths", "rays", "light_queries", "nodes", "instances", "prims", "shades"):
-            assert outs[0][2][k] == o[2][k], k
 
 
 def test_device_buffer_view_is_the_running_mean(gpu, abi, lib, cornell_abi):
