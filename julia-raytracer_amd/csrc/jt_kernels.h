@@ -372,9 +372,33 @@ struct Trav {
     int prim, nprim;   // leaf cursor: next primitive record, primitives left
     int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
     float h_u, h_v;
-    int nh;              // hits accepted so far (every tmax change), saturating at 63
+    int nh;              // bits 0-5: hits accepted so far (every tmax change), saturating at 63;
+                         // bits 8-10: where the closest hit so far was found (TIE_*, tie_ok)
     unsigned nxt;        // wide traversal: the child word visited by the next node step (W_EMPTY: pop)
 };
+
+// Exact-t ties in the near-first orders (JT_TRAVERSAL_NEAR / WIDE). The reference accepts a hit
+// at t == tmax (src/geometry.jl:226, only t > tmax rejects), so among equal-t hits the one it
+// tests LAST wins. The near-first orders visit every internal node's children in the opposite
+// order (at every level of both trees), so they reach the leaves of a tree in exactly the
+// reverse of the reference's sequence, while a leaf's primitives and a TLAS leaf's instances keep
+// their order. A tie with the closest hit so far therefore wins in the reference's order iff it
+// is in the same BLAS leaf (a later primitive), or in another instance of the same TLAS leaf (a
+// later instance); from an earlier BLAS leaf of the same instance, or an earlier TLAS leaf, the
+// hit so far is the reference's later one and stays. TIE_* record where the hit so far was found,
+// relative to the leaf / instance / TLAS leaf being visited (cleared when one starts, all set by
+// an accepted hit). The reference's own order accepts every tie.
+constexpr int TIE_LEAF = 1 << 8, TIE_INST = 2 << 8, TIE_TLEAF = 4 << 8, NH_COUNT = 63;
+__device__ __forceinline__ bool tie_ok(const DScene& S, const Trav& T) {
+    return S.order_flip == 0 || (T.nh & TIE_LEAF) || (T.nh & (TIE_INST | TIE_TLEAF)) == TIE_TLEAF;
+}
+// a hit at t (t <= tmax already) replaces the closest hit so far
+__device__ __forceinline__ bool accept_hit(const DScene& S, const Trav& T, float t) {
+    return t < T.tmax || tie_ok(S, T);
+}
+__device__ __forceinline__ void hit_accepted(Trav& T) {
+    T.nh = ((T.nh & NH_COUNT) + ((T.nh & NH_COUNT) < NH_COUNT ? 1 : 0)) | TIE_LEAF | TIE_INST | TIE_TLEAF;
+}
 
 __device__ __forceinline__ int neg_mask(v3 d, int flip) {
     return ((d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0)) ^ flip;
@@ -479,16 +503,16 @@ __device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
                                               V3(r3.x, r3.z, r4.x));
     const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.y, r0.w, r1.y), V3(r1.w, r2.y, r2.w),
                                               V3(r3.y, r3.w, r4.y));
-    if (tri_hit_before(p1, T.tmax)) {
-        T.nh += T.nh < 63 ? 1 : 0;
+    if (tri_hit_before(p1, T.tmax) && accept_hit(S, T, p1.t)) {
+        hit_accepted(T);
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.z);
         T.h_u = p1.u;
         T.h_v = p1.v;
         T.tmax = p1.t;
     }
-    if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax)) {
-        T.nh += T.nh < 63 ? 1 : 0;
+    if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax) && accept_hit(S, T, p2.t)) {
+        hit_accepted(T);
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.w);
         T.h_u = p2.u;
@@ -514,8 +538,8 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     const float4* r = S.prims + 4 * T.prim;
     const float4 a = r[0], b = r[1], c = r[2], d = r[3];
     const PrimHit p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
-    if (p.hit) {
-        T.nh += T.nh < 63 ? 1 : 0;
+    if (p.hit && accept_hit(S, T, p.t)) {
+        hit_accepted(T);
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(a.w);
         T.h_u = p.u;
@@ -585,6 +609,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         }
         T.cur_inst = (int)idx;
         T.cur_kind = ib.z;
+        T.nh &= ~TIE_INST;
         type = T_BLAS;
         idx = (unsigned)ib.x;
     } else if (XF && type == T_TLAS && T.inst_space) {
@@ -610,7 +635,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         // keep it one 16-B load: without this the compiler narrows it to the start/meta half and
         // sinks the z-slab half into the branch below (a second instruction in every mixed step)
         __asm__("" : "+v"(nb.x), "+v"(nb.y), "+v"(nb.z), "+v"(nb.w));
-        if (snap == 63u || snap != (unsigned)T.nh)
+        if (snap == 63u || snap != (unsigned)(T.nh & NH_COUNT))
             if (!intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, S.nodes[idx].a, nb)) return;
     } else {  // LDS mode (no pre-test): the whole node, two LDS reads
         const DNode nd = S.nodes[idx];
@@ -638,7 +663,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             const bool k0 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n0.a, n0.b);
             const bool k1 = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, n1.a, n1.b);
             if (COUNT) cnt.nodes += (k0 ? 0 : 1) + (k1 ? 0 : 1);
-            const unsigned ptag = type << 30 | (unsigned)T.nh << 24;  // pre-tested at hit count nh
+            const unsigned ptag = type << 30 | (unsigned)(T.nh & NH_COUNT) << 24;  // pre-tested at hit count nh
             if (k0) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_second);
             if (k1) st_push<RING, OVF>(S, T, stack, pixel, ptag | c_first);
         } else {
@@ -646,11 +671,13 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_first);
         }
     } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
+        T.nh &= ~TIE_TLEAF;
         for (int k = num - 1; k >= 0; k--)
             st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | SNAP_NONE | (unsigned)(start + k));
     } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
+        T.nh &= ~TIE_LEAF;
     }
 }
 
@@ -700,6 +727,7 @@ __device__ __forceinline__ void wide_take(Trav& T, unsigned w) {
     const bool leaf = (w & (W_LEAF | W_INST)) == W_LEAF;  // a BLAS leaf: its primitives are tested next
     T.prim = leaf ? (int)(w & W_START) : T.prim;
     T.nprim = leaf ? (int)((w >> 28) & 3u) + 1 : T.nprim;
+    T.nh = leaf ? T.nh & ~TIE_LEAF : T.nh;
     T.nxt = leaf ? T.nxt : w;  // a record, or a TLAS leaf (its first instance is visited by the next step)
 }
 // one record visit: the up-to-four child boxes against the current ray and tmax; the first passing
@@ -755,13 +783,15 @@ __device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* st
                 return;
             }
         } else {  // the rest of a TLAS leaf's instances
-            w = W_LEAF | W_INST | ((e >> 24) & 3u) << 28 | idx;
+            w = W_LEAF | W_INST | ((e >> 24) & 3u) << 28 | idx | W_CONT;
         }
     } else {
         T.nxt = W_EMPTY;
     }
     if (w & W_LEAF) {  // a TLAS leaf: visit its first instance, keep the others as a range entry
-        const unsigned inst = w & W_START, n1 = (w >> 28) & 3u;
+        // (W_CONT: a later instance of the TLAS leaf being visited)
+        T.nh &= (w & W_CONT) ? ~TIE_INST : ~(TIE_INST | TIE_TLEAF);
+        const unsigned inst = w & W_START & ~W_CONT, n1 = (w >> 28) & 3u;
         if (n1) st_push<RING, OVF>(S, T, stack, pixel, W_LEAF | (n1 - 1u) << 24 | (inst + 1u));
         if (COUNT) cnt.instances++;
         const int4 ib = S.inst_blas[inst];  // wide BLAS root record, identity, kind, shape
@@ -1853,8 +1883,9 @@ __global__ __launch_bounds__(BLOCK) JT_WAVES_PER_EU_F(F) void trace_kernel_lds(D
 // LDSK: the specialisation also has an LDS-mode kernel (the large-scene masks run in HBM mode).
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool LDSK, bool WIDE>
 hipError_t launch_t(const DScene& S, const DParams& P, int s0, int s1, const DAccum& A, hipStream_t st, int cus) {
-    const int tiles = launch_tiles(P);
-    const int want = (tiles + BLOCK / 64 - 1) / (BLOCK / 64);
+    // one wave per work unit (tile, stream slot) at most
+    const long long units = (long long)launch_tiles(P) * std::min(s1 - s0, 1 << P.lk);
+    const int want = (int)std::min<long long>((units + BLOCK / 64 - 1) / (BLOCK / 64), 1 << 30);
     if (want == 0) return hipSuccess;  // a multi-device share without tiles (tiny image)
     int per_cu = 0;
     hipError_t e;

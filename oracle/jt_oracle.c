@@ -328,7 +328,7 @@ typedef struct {
 typedef struct { int n, cap; wrec_t* r; } wtree_t;
 
 /* ---------------------------------------------------------- scene view */
-typedef struct {
+typedef struct ctx_s {
     const jt_scene* scene;
     const jt_scene_bvh* bvh;
     const jt_lights* lights;
@@ -350,6 +350,10 @@ typedef struct {
     int stack_size;
     int overflow;
     or_counters cnt;
+    /* or_order_diff (diagnostic): the same scene query in another traversal order, compared */
+    const struct ctx_s* alt;
+    uint64_t diag[10];
+    int path_diff;
 } scratch_t;
 
 static inline v3 pos3(const jt_shape* s, int32_t v) {
@@ -367,9 +371,23 @@ static inline v4 col4(const jt_shape* s, int32_t v) {
 typedef struct { int element; v2 uv; float distance; int hit; } shape_isec;
 typedef struct { int instance, element; v2 uv; float distance; int hit; } scene_isec;
 
-/* intersect_shape_bvh (src/bvh.jl:373-491), find_any = false */
-static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, scratch_t* sc) {
+/* Exact-t ties in the near-first orders (the build's JT_TRAVERSAL_NEAR / WIDE, include/jtrace.h).
+ * The reference accepts a hit at t == tmax (src/geometry.jl:226), so among equal-t hits the one
+ * it tests last wins. The near-first orders visit every internal node's children in the opposite
+ * order, so they reach a tree's leaves in the reverse of the reference's sequence, while a leaf's
+ * primitives and a TLAS leaf's instances keep their order: an equal-t hit replaces the hit so far
+ * iff it is in the same BLAS leaf, or in a later instance of the same TLAS leaf (`outer_ok`). The
+ * reference's own order accepts every tie. */
+static inline int near_order(const ctx_t* c) { return c->params->traversal != JT_TRAVERSAL_REFERENCE; }
+static inline int take_hit(const ctx_t* c, const prim_isec* p, float tmax, int in_leaf, int in_inst, int outer_ok) {
+    return p->hit && (p->distance < tmax || !near_order(c) || in_leaf || (!in_inst && outer_ok));
+}
+
+/* intersect_shape_bvh (src/bvh.jl:373-491), find_any = false; outer_ok: the ray's tmax is a hit
+ * of an earlier instance of the TLAS leaf being visited (ties with it are won, see take_hit) */
+static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, scratch_t* sc, int outer_ok) {
     shape_isec isec = {-1, {0, 0}, 0, 0};
+    int in_inst = 0, in_leaf;
     const jt_bvh_tree* bvh = &c->bvh->blas[shape_id];
     const jt_shape* shape = &c->scene->shapes[shape_id];
     if (bvh->nnodes == 0) return isec;
@@ -394,12 +412,14 @@ static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, sc
                 stack[node_cur++] = node->start;
             }
         } else if (shape->ntriangles > 0) {
+            in_leaf = 0;
             for (int i = node->start; i < node->start + node->num; i++) {
                 int e = bvh->primitives[i];
                 const int32_t* t = &shape->triangles[3 * e];
                 sc->cnt.prims++;
                 prim_isec p = intersect_triangle(&ray, pos3(shape, t[0]), pos3(shape, t[1]), pos3(shape, t[2]));
-                if (!p.hit) continue;
+                if (!take_hit(c, &p, ray.tmax, in_leaf, in_inst, outer_ok)) continue;
+                in_leaf = in_inst = 1;
                 isec.element = e;
                 isec.uv = p.uv;
                 isec.distance = p.distance;
@@ -407,13 +427,15 @@ static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, sc
                 ray.tmax = p.distance;
             }
         } else if (shape->nquads > 0) {
+            in_leaf = 0;
             for (int i = node->start; i < node->start + node->num; i++) {
                 int e = bvh->primitives[i];
                 const int32_t* q = &shape->quads[4 * e];
                 sc->cnt.prims++;
                 prim_isec p = intersect_quad(&ray, pos3(shape, q[0]), pos3(shape, q[1]), pos3(shape, q[2]),
                                              pos3(shape, q[3]));
-                if (!p.hit) continue;
+                if (!take_hit(c, &p, ray.tmax, in_leaf, in_inst, outer_ok)) continue;
+                in_leaf = in_inst = 1;
                 isec.element = e;
                 isec.uv = p.uv;
                 isec.distance = p.distance;
@@ -458,13 +480,15 @@ static scene_isec intersect_scene_bvh(const ctx_t* c, ray3 ray, scratch_t* sc) {
                 stack[node_cur++] = node->start;
             }
         } else {
+            int in_tleaf = 0;  /* the hit so far is from an earlier instance of this TLAS leaf */
             for (int i = node->start; i < node->start + node->num; i++) {
                 int inst_id = bvh->primitives[i];
                 const jt_instance* inst = &c->scene->instances[inst_id];
                 sc->cnt.instances++;
                 ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], &ray);
-                shape_isec s = intersect_shape_bvh(c, inst->shape, inv_ray, sc);
+                shape_isec s = intersect_shape_bvh(c, inst->shape, inv_ray, sc, in_tleaf);
                 if (!s.hit) continue;
+                in_tleaf = 1;
                 isec.instance = inst_id;
                 isec.element = s.element;
                 isec.uv = s.uv;
@@ -484,7 +508,7 @@ static scene_isec intersect_instance_bvh(const ctx_t* c, int inst_id, ray3 ray, 
     sc->cnt.light_queries++;
     sc->cnt.instances++;
     ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], &ray);
-    shape_isec s = intersect_shape_bvh(c, inst->shape, inv_ray, sc);
+    shape_isec s = intersect_shape_bvh(c, inst->shape, inv_ray, sc, 0);
     if (!s.hit) return isec;
     isec.instance = inst_id;
     isec.element = s.element;
@@ -609,7 +633,7 @@ static void w_test(const wrec_t* w, const ray3* ray, v3 dinv, int* hit) {
     }
 }
 static void w_shape(const ctx_t* c, int shape_id, int r, ray3* ray, v3 dinv, const int* dsign, shape_isec* isec,
-                    scratch_t* sc) {
+                    scratch_t* sc, int outer_ok, int* in_inst) {
     const jt_bvh_tree* bvh = &c->bvh->blas[shape_id];
     const jt_shape* shape = &c->scene->shapes[shape_id];
     const wrec_t* w = &c->wblas[shape_id].r[r];
@@ -622,9 +646,10 @@ static void w_shape(const ctx_t* c, int shape_id, int r, ray3* ray, v3 dinv, con
         if (!hit[k]) continue;
         const jt_bvh_node* node = &bvh->nodes[w->child[k]];
         if (node->internal) {
-            w_shape(c, shape_id, w->rec[k], ray, dinv, dsign, isec, sc);
+            w_shape(c, shape_id, w->rec[k], ray, dinv, dsign, isec, sc, outer_ok, in_inst);
             continue;
         }
+        int in_leaf = 0;
         for (int i = node->start; i < node->start + node->num; i++) {
             int e = bvh->primitives[i];
             prim_isec p;
@@ -636,7 +661,8 @@ static void w_shape(const ctx_t* c, int shape_id, int r, ray3* ray, v3 dinv, con
                 const int32_t* q4 = &shape->quads[4 * e];
                 p = intersect_quad(ray, pos3(shape, q4[0]), pos3(shape, q4[1]), pos3(shape, q4[2]), pos3(shape, q4[3]));
             }
-            if (!p.hit) continue;
+            if (!take_hit(c, &p, ray->tmax, in_leaf, *in_inst, outer_ok)) continue;
+            in_leaf = *in_inst = 1;
             isec->element = e;
             isec->uv = p.uv;
             isec->distance = p.distance;
@@ -646,11 +672,12 @@ static void w_shape(const ctx_t* c, int shape_id, int r, ray3* ray, v3 dinv, con
     }
 }
 /* intersect_shape_bvh on the wide records */
-static shape_isec intersect_shape_wide(const ctx_t* c, int shape_id, ray3 ray, scratch_t* sc) {
+static shape_isec intersect_shape_wide(const ctx_t* c, int shape_id, ray3 ray, scratch_t* sc, int outer_ok) {
     shape_isec isec = {-1, {0, 0}, 0, 0};
     v3 dinv = V3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
     int dsign[3] = {(ray.d.x < 0) ^ 1, (ray.d.y < 0) ^ 1, (ray.d.z < 0) ^ 1};
-    w_shape(c, shape_id, 0, &ray, dinv, dsign, &isec, sc);
+    int in_inst = 0;
+    w_shape(c, shape_id, 0, &ray, dinv, dsign, &isec, sc, outer_ok, &in_inst);
     return isec;
 }
 static void w_scene(const ctx_t* c, int r, ray3* ray, v3 dinv, const int* dsign, scene_isec* isec, scratch_t* sc) {
@@ -668,12 +695,14 @@ static void w_scene(const ctx_t* c, int r, ray3* ray, v3 dinv, const int* dsign,
             w_scene(c, w->rec[k], ray, dinv, dsign, isec, sc);
             continue;
         }
+        int in_tleaf = 0;
         for (int i = node->start; i < node->start + node->num; i++) {
             int inst_id = bvh->primitives[i];
             sc->cnt.instances++;
             ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], ray);
-            shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc);
+            shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc, in_tleaf);
             if (!s.hit) continue;
+            in_tleaf = 1;
             isec->instance = inst_id;
             isec->element = s.element;
             isec->uv = s.uv;
@@ -699,7 +728,7 @@ static scene_isec intersect_instance_wide(const ctx_t* c, int inst_id, ray3 ray,
     sc->cnt.light_queries++;
     sc->cnt.instances++;
     ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], &ray);
-    shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc);
+    shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc, 0);
     if (!s.hit) return isec;
     isec.instance = inst_id;
     isec.element = s.element;
@@ -709,8 +738,28 @@ static scene_isec intersect_instance_wide(const ctx_t* c, int inst_id, ray3 ray,
     return isec;
 }
 /* the traversal jt_params.traversal selects */
-static scene_isec scene_query(const ctx_t* c, ray3 ray, scratch_t* sc) {
+static scene_isec scene_query1(const ctx_t* c, ray3 ray, scratch_t* sc) {
     return c->params->traversal == JT_TRAVERSAL_WIDE ? intersect_scene_wide(c, ray, sc) : intersect_scene_bvh(c, ray, sc);
+}
+/* or_order_diff: classify the other order's closest hit against this one's, per query */
+static void order_diff(const ctx_t* alt, ray3 ray, scene_isec r, scratch_t* sc) {
+    scratch_t tmp = *sc;
+    tmp.alt = NULL;
+    scene_isec a = scene_query1(alt, ray, &tmp);
+    sc->overflow |= tmp.overflow;
+    sc->diag[0]++;
+    int k;
+    if (r.hit != a.hit) k = a.hit ? 3 : 4;                                       /* one order misses */
+    else if (!r.hit || (r.instance == a.instance && r.element == a.element)) k = 1; /* same hit */
+    else if (r.distance == a.distance) k = 2;                                    /* exact-t tie */
+    else k = a.distance < r.distance ? 5 : 6;                                    /* different t */
+    sc->diag[k]++;
+    if (k != 1) sc->path_diff = 1;
+}
+static scene_isec scene_query(const ctx_t* c, ray3 ray, scratch_t* sc) {
+    scene_isec r = scene_query1(c, ray, sc);
+    if (sc->alt) order_diff(sc->alt, ray, r, sc);
+    return r;
 }
 static scene_isec instance_query(const ctx_t* c, int inst_id, ray3 ray, scratch_t* sc) {
     return c->params->traversal == JT_TRAVERSAL_WIDE ? intersect_instance_wide(c, inst_id, ray, sc)
@@ -1776,6 +1825,10 @@ static void trace_pixel(worker_t* w, int i, int j) {
         if (params->sampler == JT_SAMPLER_NAIVE) r = trace_naive(c, ray, &rng, &w->sc);
         else r = trace_path(c, ray, &rng, &w->sc);
         w->sc.cnt.paths++;
+        if (w->sc.path_diff) {
+            w->sc.diag[7]++;
+            w->sc.path_diff = 0;
+        }
         v3 radiance = r.radiance;
         if (!isfinite3(radiance)) radiance = V3(0, 0, 0);
         float mr = max3f(radiance);
@@ -1906,17 +1959,62 @@ static void free_ctx(ctx_t* c) {
     free(c->wblas);
 }
 
+static int trace_rows_impl(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
+                           const jt_params* params, int32_t width, int32_t height, int32_t row0, int32_t row1,
+                           int32_t first, int32_t s0, int32_t s1, float* image, float* albedo, float* normal,
+                           int64_t* hits, int32_t lk, float* part_img, float* part_alb, float* part_nrm,
+                           int64_t* part_hits, int32_t nthreads, or_counters* counters, const jt_params* alt_params,
+                           uint64_t* diag);
 int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights, const jt_params* params,
                   int32_t width, int32_t height, int32_t row0, int32_t row1, int32_t first, int32_t s0, int32_t s1,
                   float* image, float* albedo, float* normal, int64_t* hits, int32_t lk, float* part_img,
                   float* part_alb, float* part_nrm, int64_t* part_hits, int32_t nthreads, or_counters* counters) {
+    return trace_rows_impl(scene, bvh, lights, params, width, height, row0, row1, first, s0, s1, image, albedo, normal,
+                           hits, lk, part_img, part_alb, part_nrm, part_hits, nthreads, counters, NULL, NULL);
+}
+
+/* Diagnostic (tests/test_oracle_traversal.py): trace samples [s0, s1) of every pixel in
+ * params->traversal and, at every closest-hit scene query, also run the query in alt_traversal
+ * on the same ray. diag[0] queries, [1] same hit, [2] another primitive at exactly the same t,
+ * [3] only the alternative order hits, [4] only this order hits, [5] the alternative's hit is
+ * closer, [6] farther, [7] paths with at least one differing query. */
+int or_order_diff(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights, const jt_params* params,
+                  int32_t alt_traversal, int32_t width, int32_t height, int32_t s0, int32_t s1, int32_t nthreads,
+                  uint64_t* diag) {
+    jt_params alt = *params;
+    alt.traversal = alt_traversal;
+    size_t np = (size_t)width * height;
+    float* im = (float*)calloc(np * 4, sizeof(float));
+    float* al = (float*)calloc(np * 3, sizeof(float));
+    float* nm = (float*)calloc(np * 3, sizeof(float));
+    int64_t* h = (int64_t*)calloc(np, sizeof(int64_t));
+    int st = (im && al && nm && h) ? trace_rows_impl(scene, bvh, lights, params, width, height, 0, height, s0, s0, s1, im, al,
+                                                     nm, h, 0, NULL, NULL, NULL, NULL, nthreads, NULL, &alt, diag)
+                                   : JT_ERR_NOMEM;
+    free(im);
+    free(al);
+    free(nm);
+    free(h);
+    return st;
+}
+
+static int trace_rows_impl(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
+                           const jt_params* params, int32_t width, int32_t height, int32_t row0, int32_t row1,
+                           int32_t first, int32_t s0, int32_t s1, float* image, float* albedo, float* normal,
+                           int64_t* hits, int32_t lk, float* part_img, float* part_alb, float* part_nrm,
+                           int64_t* part_hits, int32_t nthreads, or_counters* counters, const jt_params* alt_params,
+                           uint64_t* diag) {
     if (!scene || !bvh || !lights || !params || !image || !albedo || !normal || !hits) return JT_ERR_INVALID;
     if (lk < 0 || lk > 6 || (lk > 0 && (!part_img || !part_alb || !part_nrm || !part_hits))) return JT_ERR_INVALID;
     if (width <= 0 || height <= 0 || s0 < first || s1 < s0 || row0 < 0 || row1 > height) return JT_ERR_INVALID;
     if (nthreads < 1) nthreads = 1;
-    ctx_t c;
+    ctx_t c, alt;
     int st = setup_ctx(&c, scene, bvh, lights, params, width, height);
     if (st != JT_OK) { free_ctx(&c); return st; }
+    if (alt_params) {
+        st = setup_ctx(&alt, scene, bvh, lights, alt_params, width, height);
+        if (st != JT_OK) { free_ctx(&alt); free_ctx(&c); return st; }
+    }
     worker_t* ws = (worker_t*)calloc((size_t)nthreads, sizeof(worker_t));
     pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
     int ssize = params->bvhstacksize > 0 ? params->bvhstacksize : 128;
@@ -1939,6 +2037,7 @@ int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_light
         w->part_alb = part_alb;
         w->part_nrm = part_nrm;
         w->part_hits = part_hits;
+        w->sc.alt = alt_params ? &alt : NULL;
         w->sc.stack = (int32_t*)malloc(sizeof(int32_t) * (size_t)ssize);
         w->sc.sub_stack = (int32_t*)malloc(sizeof(int32_t) * (size_t)ssize);
         w->sc.stack_size = ssize;
@@ -1961,6 +2060,8 @@ int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_light
         total.instances += w->sc.cnt.instances;
         total.prims += w->sc.cnt.prims;
         total.shades += w->sc.cnt.shades;
+        if (diag)
+            for (int k = 0; k < 10; k++) diag[k] += w->sc.diag[k];
         free(w->sc.stack);
         free(w->sc.sub_stack);
     }
@@ -1968,6 +2069,7 @@ int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_light
     free(ws);
     free(th);
     free_ctx(&c);
+    if (alt_params) free_ctx(&alt);
     return overflow ? JT_ERR_STACK : JT_OK;
 }
 

@@ -35,6 +35,9 @@ def _load(abi):
                                   C.POINTER(abi.jt_params), C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                   C.c_int32, C.c_int32, C.c_int32, f32p, f32p, f32p, i64p, C.c_int32,
                                   f32p, f32p, f32p, i64p, C.c_int32, C.POINTER(Counters)]
+    lib.or_order_diff.argtypes = [C.POINTER(abi.jt_scene), C.POINTER(abi.jt_scene_bvh), C.POINTER(abi.jt_lights),
+                                  C.POINTER(abi.jt_params), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                  C.c_int32, C.POINTER(C.c_uint64)]
     lib.or_intersect_triangle.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p, f32p, f32p]
     lib.or_intersect_bbox.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p]
     lib.or_fresnel_dielectric.argtypes = [C.c_float, f32p, f32p]
@@ -135,6 +138,20 @@ class Oracle:
         if st != 0:
             raise RuntimeError(f"oracle trace failed: {st}")
         return image, albedo, normal, hits, cnt.as_dict()
+
+
+    def order_diff(self, scene_abi, bvh, lights, params, alt_traversal, width, height, s0, s1, nthreads=None):
+        """Diagnostic: trace [s0, s1) in params.traversal and compare every closest-hit scene query
+        with the same query in alt_traversal (oracle/jt_oracle.c or_order_diff)."""
+        if nthreads is None:
+            nthreads = min(16, os.cpu_count() or 1)
+        d = (C.c_uint64 * 10)()
+        st = self.lib.or_order_diff(scene_abi.ref, C.byref(bvh.struct), C.byref(lights.struct), C.byref(params),
+                                    alt_traversal, width, height, s0, s1, nthreads, d)
+        if st != 0:
+            raise RuntimeError(f"oracle order_diff failed: {st}")
+        keys = ("queries", "same", "tie", "alt_only_hit", "ref_only_hit", "alt_closer", "alt_farther", "paths_differing")
+        return {k: int(d[i]) for i, k in enumerate(keys)}
 
 
 class _Owned:
