@@ -11,6 +11,7 @@
 #   sig:<w>                    write workload <w>'s one-GPU image signature (bench --write-signature)
 #   ab:<w>:<lib>,<lib>...      A/B of library builds (build/libjtrace_hip[_<lib>].so, "base" = the
 #                              product build), each twice, interleaved
+#   prof:<w>                   rocprofv3 --kernel-trace --stats of a short bench run of workload <w>
 #   stamps:<w>                 the JT_STAMPS build's per-phase wave clocks (scripts/stamps.py)
 #   host                       the box's CPU description
 # workloads: cb (the headline, cornellbox path 1280x720x256), cb1 (config 1: naive 256x256x16),
@@ -91,6 +92,8 @@ for task in "$@"; do
                     echo "$w $lib rep$rep => $(grep -h '"value"' "$O/ab_${name}_${lib}_$rep.log" | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print(round(d["value"],1))')" | tee -a "$O/ab_summary.txt"
                 done
             done ;;
+        prof)
+            $S 300 "$O/prof_$name.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$name" -o kt -- python3 bench.py --no-cpu-baseline --no-reference-order $(wargs "$w") --steps 2 --warmup 1 || exit 1 ;;
         stamps)
             $S 400 "$O/stamps_$name.log" python scripts/stamps.py $(wargs "$w") || exit 1 ;;
         host)
