@@ -173,6 +173,8 @@ struct DScene {
     const float* srgb_lut;  // srgb_to_rgb(byte_to_float(b)), 256 entries (src/color.jl:12-23)
     const float* byte_lut;  // byte_to_float(b)
     int tlas_nnodes, nenvs, nlights;
+    const int2* flat;  // (instance, record) of every primitive record of every instance (JT_FLAT)
+    int nflat;
     int order_flip;  // jt_params.traversal: 0 the reference's child order, 7 the near child first
                      // (near and wide)
     float light_pick_pdf;  // sample_uniform_pdf(nlights) = Float32(1 / nlights) (src/sampling.jl:31)

@@ -812,6 +812,35 @@ __device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* st
     }
     wide_visit<RING, OVF, COUNT>(S, T, stack, pixel, cnt, w);
 }
+// JT_FLAT (experiment): a small scene's closest-hit query tests every primitive record of every
+// instance at once (uniform control, every lane of the wave together), FT_NONE scenes only
+#ifndef JT_FLAT
+#define JT_FLAT 0
+#endif
+template <int F>
+__device__ __forceinline__ void flat_query(const DScene& S, Trav& T, v3 o, v3 d) {
+    T.wo = o;
+    T.wd = d;
+    T.lo = o;
+    T.ld = d;
+    T.tmax = __builtin_inff();
+    T.nh = 0;
+    T.h_inst = -1;
+    T.h_elem = -1;
+    T.h_u = 0;
+    T.h_v = 0;
+    T.nprim = 0;
+    T.sp = 0;
+    T.nxt = W_EMPTY;
+    for (int k = 0; k < S.nflat; k++) {
+        const int2 ir = S.flat[k];
+        T.cur_inst = ir.x;
+        T.prim = ir.y;
+        T.nprim = 2;
+        tri_pair<F>(S, T, 0);
+    }
+    T.nprim = 0;
+}
 // a node step in either traversal
 template <bool WIDE, int RING, bool OVF, int COUNT, bool NCACHE, int F>
 __device__ __forceinline__ void node_step_any(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt) {
@@ -1570,7 +1599,8 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
             const int pixel = item_pixel(item, P, tiles_x);
             if (!ft_none(F)) acc[12 * BLOCK] = stream_weight(P, sample);
             start_path<F>(P, pixel % P.width, pixel / P.width, pixel, sample, st);
-            query_start<WIDE>(S, T, st.o, st.d, -1, stack);
+            if constexpr (JT_FLAT && ft_none(F) && !WIDE) flat_query<F>(S, T, st.o, st.d);
+            else query_start<WIDE>(S, T, st.o, st.d, -1, stack);
             if (!WC) lds_count(1, true);
             if constexpr (item_first_pop<WIDE, F>()) {
 #pragma unroll
@@ -1761,7 +1791,8 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 } else {
                     if (WC) c_ray = true;
                     else lds_count(1, true);
-                    query_start<WIDE>(S, T, st.o, st.d, -1, stack);
+                    if constexpr (JT_FLAT && ft_none(F) && !WIDE) flat_query<F>(S, T, st.o, st.d);
+                    else query_start<WIDE>(S, T, st.o, st.d, -1, stack);
                 }
                 // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
                 // where most of the wave's lanes take part, rather than in a sparser traversal step
