@@ -56,9 +56,6 @@ struct alignas(16) DWide {
     uint4 r1, r2, r3;
 };
 enum : unsigned { W_EMPTY = 0xffffffffu, W_LEAF = 0x80000000u, W_INST = 0x40000000u, W_START = 0x0fffffffu };
-// in the kernel, a TLAS leaf's instance word taken from its range entry (a later instance of the
-// leaf being visited) carries W_CONT (instances are below 2^24, so bit 27 of the start is free)
-constexpr unsigned W_CONT = 0x08000000u;
 // Traversal record of an instance, 64 B: inverse(frame, true) as 12 floats + ids.
 struct alignas(16) DInstTrav {
     float4 i0, i1, i2;  // inv x.xyz y.x | y.yz z.xy | z.z o.xyz
@@ -173,6 +170,8 @@ struct DScene {
     const float* srgb_lut;  // srgb_to_rgb(byte_to_float(b)), 256 entries (src/color.jl:12-23)
     const float* byte_lut;  // byte_to_float(b)
     int tlas_nnodes, nenvs, nlights;
+    const int* inst_tleaf;  // per instance: the first instance of its TLAS leaf (the near-first
+                            // orders' tie decision, jtk::tie_ok; read only at an exact-t tie)
     const int2* flat;  // (instance, record) of every primitive record of every instance (JT_FLAT)
     int nflat;
     int order_flip;  // jt_params.traversal: 0 the reference's child order, 7 the near child first

@@ -373,7 +373,7 @@ struct Trav {
     int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
     float h_u, h_v;
     int nh;              // bits 0-5: hits accepted so far (every tmax change), saturating at 63;
-                         // bits 8-10: where the closest hit so far was found (TIE_*, tie_ok)
+                         // bit 8 (quad scenes): the closest hit so far is in the current leaf (TIE_LEAF)
     unsigned nxt;        // wide traversal: the child word visited by the next node step (W_EMPTY: pop)
 };
 
@@ -385,20 +385,25 @@ struct Trav {
 // their order. A tie with the closest hit so far therefore wins in the reference's order iff it
 // is in the same BLAS leaf (a later primitive), or in another instance of the same TLAS leaf (a
 // later instance); from an earlier BLAS leaf of the same instance, or an earlier TLAS leaf, the
-// hit so far is the reference's later one and stays. TIE_* record where the hit so far was found,
-// relative to the leaf / instance / TLAS leaf being visited (cleared when one starts, all set by
-// an accepted hit). The reference's own order accepts every tie.
-constexpr int TIE_LEAF = 1 << 8, TIE_INST = 2 << 8, TIE_TLEAF = 4 << 8, NH_COUNT = 63;
-__device__ __forceinline__ bool tie_ok(const DScene& S, const Trav& T) {
-    return S.order_flip == 0 || (T.nh & TIE_LEAF) || (T.nh & (TIE_INST | TIE_TLEAF)) == TIE_TLEAF;
+// hit so far is the reference's later one and stays. Ties are rare (2e-5 of bathroom1's queries,
+// none on cornellbox), so the decision is made only at a tie: the same leaf is known to the
+// primitive step (a triangle leaf, <= 4 primitives, is tested within one step; a quad leaf keeps
+// TIE_LEAF in nh), the same instance from the hit's instance, the same TLAS leaf from a per-
+// instance table (DScene::inst_tleaf). The reference's own order accepts every tie.
+#ifndef JT_TIE
+#define JT_TIE 1
+#endif
+constexpr int TIE_LEAF = 1 << 8, NH_COUNT = 63;
+__device__ __forceinline__ bool tie_ok(const DScene& S, const Trav& T, bool same_leaf) {
+    if (!JT_TIE || S.order_flip == 0 || same_leaf) return true;
+    if (T.h_inst == T.cur_inst) return false;  // an earlier BLAS leaf of this instance
+    return S.inst_tleaf[T.h_inst] == S.inst_tleaf[T.cur_inst];  // an earlier instance of this TLAS leaf
 }
 // a hit at t (t <= tmax already) replaces the closest hit so far
-__device__ __forceinline__ bool accept_hit(const DScene& S, const Trav& T, float t) {
-    return t < T.tmax || tie_ok(S, T);
+__device__ __forceinline__ bool accept_hit(const DScene& S, const Trav& T, float t, bool same_leaf) {
+    return t < T.tmax || tie_ok(S, T, same_leaf);
 }
-__device__ __forceinline__ void hit_accepted(Trav& T) {
-    T.nh = ((T.nh & NH_COUNT) + ((T.nh & NH_COUNT) < NH_COUNT ? 1 : 0)) | TIE_LEAF | TIE_INST | TIE_TLEAF;
-}
+__device__ __forceinline__ void hit_count(Trav& T) { T.nh += (T.nh & NH_COUNT) < NH_COUNT ? 1 : 0; }
 
 __device__ __forceinline__ int neg_mask(v3 d, int flip) {
     return ((d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0)) ^ flip;
@@ -496,23 +501,25 @@ __device__ __forceinline__ void query_start(const DScene& S, Trav& T, v3 o, v3 d
 // the two triangles' components interleaved, 5 loads instead of 6 for two separate records).
 // k is 0 or 2.
 template <int F>
-__device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
+__device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k, bool& leaf_hit) {
     const float4* r = S.prims + 5 * (T.prim + (k >> 1));
     const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
     const PrimHit p1 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.x, r0.z, r1.x), V3(r1.z, r2.x, r2.z),
                                               V3(r3.x, r3.z, r4.x));
     const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.y, r0.w, r1.y), V3(r1.w, r2.y, r2.w),
                                               V3(r3.y, r3.w, r4.y));
-    if (tri_hit_before(p1, T.tmax) && accept_hit(S, T, p1.t)) {
-        hit_accepted(T);
+    if (tri_hit_before(p1, T.tmax) && accept_hit(S, T, p1.t, leaf_hit)) {
+        hit_count(T);
+        leaf_hit = true;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.z);
         T.h_u = p1.u;
         T.h_v = p1.v;
         T.tmax = p1.t;
     }
-    if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax) && accept_hit(S, T, p2.t)) {
-        hit_accepted(T);
+    if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax) && accept_hit(S, T, p2.t, leaf_hit)) {
+        hit_count(T);
+        leaf_hit = true;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.w);
         T.h_u = p2.u;
@@ -523,10 +530,12 @@ __device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
 template <int COUNT, int F>
 __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cnt) {
     if (!(F & FT_QUAD) || T.cur_kind == KIND_TRI) {
-        tri_pair<F>(S, T, 0);
+        // a triangle leaf (<= 4 primitives, BVH_MAX_PRIMS, src/bvh.jl:32) is tested within this step
+        bool leaf_hit = false;
+        tri_pair<F>(S, T, 0, leaf_hit);
         const bool more = T.nprim > 2;
         if (__builtin_amdgcn_ballot_w64(more)) {
-            if (more) tri_pair<F>(S, T, 2);
+            if (more) tri_pair<F>(S, T, 2, leaf_hit);
         }
         const int n = T.nprim < 4 ? T.nprim : 4;
         if (COUNT) cnt.prims += n;
@@ -538,8 +547,9 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     const float4* r = S.prims + 4 * T.prim;
     const float4 a = r[0], b = r[1], c = r[2], d = r[3];
     const PrimHit p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
-    if (p.hit && accept_hit(S, T, p.t)) {
-        hit_accepted(T);
+    if (p.hit && accept_hit(S, T, p.t, (T.nh & TIE_LEAF) != 0)) {
+        hit_count(T);
+        T.nh |= TIE_LEAF;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(a.w);
         T.h_u = p.u;
@@ -609,7 +619,6 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
         }
         T.cur_inst = (int)idx;
         T.cur_kind = ib.z;
-        T.nh &= ~TIE_INST;
         type = T_BLAS;
         idx = (unsigned)ib.x;
     } else if (XF && type == T_TLAS && T.inst_space) {
@@ -671,13 +680,12 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             st_push<RING, OVF>(S, T, stack, pixel, tag | c_first);
         }
     } else if (!blas) {  // TLAS leaf: instances start .. start+num-1, in order
-        T.nh &= ~TIE_TLEAF;
         for (int k = num - 1; k >= 0; k--)
             st_push<RING, OVF>(S, T, stack, pixel, (T_INST << 30) | SNAP_NONE | (unsigned)(start + k));
     } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
-        T.nh &= ~TIE_LEAF;
+        if (F & FT_QUAD) T.nh &= ~TIE_LEAF;
     }
 }
 
@@ -723,16 +731,17 @@ __device__ __forceinline__ bool slab_test(float mx, float Mx, float my, float My
 // (Every field is written on both paths: as two branches storing to different fields, the
 // compiler merged the stores into one through a selected address, and the Trav fields it addressed
 // no longer fit in registers — they lived in scratch, stored per node step.)
+template <int F>
 __device__ __forceinline__ void wide_take(Trav& T, unsigned w) {
     const bool leaf = (w & (W_LEAF | W_INST)) == W_LEAF;  // a BLAS leaf: its primitives are tested next
     T.prim = leaf ? (int)(w & W_START) : T.prim;
     T.nprim = leaf ? (int)((w >> 28) & 3u) + 1 : T.nprim;
-    T.nh = leaf ? T.nh & ~TIE_LEAF : T.nh;
+    if (F & FT_QUAD) T.nh = leaf ? T.nh & ~TIE_LEAF : T.nh;
     T.nxt = leaf ? T.nxt : w;  // a record, or a TLAS leaf (its first instance is visited by the next step)
 }
 // one record visit: the up-to-four child boxes against the current ray and tmax; the first passing
 // child (visit order) is taken at once, the others are pushed as one group entry
-template <int RING, bool OVF, int COUNT>
+template <int RING, bool OVF, int COUNT, int F>
 __device__ __forceinline__ void wide_visit(const DScene& S, Trav& T, int* stack, int pixel, Counters& cnt, unsigned idx) {
     if (COUNT) cnt.nodes++;
     const DWide& rec = S.wnodes[idx];
@@ -759,7 +768,7 @@ __device__ __forceinline__ void wide_visit(const DScene& S, Trav& T, int* stack,
     const int k0 = __builtin_ctz(vm);
     const unsigned rest = vm & (vm - 1u);
     if (rest) st_push<RING, OVF>(S, T, stack, pixel, flips << 28 | rest << 24 | idx);
-    wide_take(T, wide_word(r3, wide_slot(flips, k0)));
+    wide_take<F>(T, wide_word(r3, wide_slot(flips, k0)));
 }
 // One node step of the wide traversal: the pending child word, or the next child of the group on
 // top of the stack (its word: one 4-B load), or the next instance of a range. An instance visit
@@ -779,19 +788,17 @@ __device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* st
             if (XF && T.inst_space && idx < (unsigned)S.tlas_wnodes) world_ray(S, T);  // back in the TLAS
             w = reinterpret_cast<const unsigned*>(S.wnodes + idx)[12 + wide_slot((e >> 28) & 7u, __builtin_ctz(m))];
             if ((w & (W_LEAF | W_INST)) == W_LEAF) {
-                wide_take(T, w);
+                wide_take<F>(T, w);
                 return;
             }
         } else {  // the rest of a TLAS leaf's instances
-            w = W_LEAF | W_INST | ((e >> 24) & 3u) << 28 | idx | W_CONT;
+            w = W_LEAF | W_INST | ((e >> 24) & 3u) << 28 | idx;
         }
     } else {
         T.nxt = W_EMPTY;
     }
     if (w & W_LEAF) {  // a TLAS leaf: visit its first instance, keep the others as a range entry
-        // (W_CONT: a later instance of the TLAS leaf being visited)
-        T.nh &= (w & W_CONT) ? ~TIE_INST : ~(TIE_INST | TIE_TLEAF);
-        const unsigned inst = w & W_START & ~W_CONT, n1 = (w >> 28) & 3u;
+        const unsigned inst = w & W_START, n1 = (w >> 28) & 3u;
         if (n1) st_push<RING, OVF>(S, T, stack, pixel, W_LEAF | (n1 - 1u) << 24 | (inst + 1u));
         if (COUNT) cnt.instances++;
         const int4 ib = S.inst_blas[inst];  // wide BLAS root record, identity, kind, shape
@@ -810,7 +817,7 @@ __device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* st
         T.cur_kind = ib.z;
         w = (unsigned)ib.x;
     }
-    wide_visit<RING, OVF, COUNT>(S, T, stack, pixel, cnt, w);
+    wide_visit<RING, OVF, COUNT, F>(S, T, stack, pixel, cnt, w);
 }
 // JT_FLAT (experiment): a small scene's closest-hit query tests every primitive record of every
 // instance at once (uniform control, every lane of the wave together), FT_NONE scenes only
@@ -837,7 +844,8 @@ __device__ __forceinline__ void flat_query(const DScene& S, Trav& T, v3 o, v3 d)
         T.cur_inst = ir.x;
         T.prim = ir.y;
         T.nprim = 2;
-        tri_pair<F>(S, T, 0);
+        bool lh = false;
+        tri_pair<F>(S, T, 0, lh);
     }
     T.nprim = 0;
 }

@@ -408,6 +408,8 @@ int check_tree(const jt_bvh_tree& t, int nprims_expected, const char* what) {
             if (n.start < 0 || n.start + 1 >= t.nnodes) return jt::fail(JT_ERR_INVALID, std::string(what) + ": bad child index");
         } else if (n.start < 0 || n.num < 0 || n.start + n.num > t.nprimitives) {
             return jt::fail(JT_ERR_INVALID, std::string(what) + ": bad leaf range");
+        } else if (n.num > 4) {  // make_bvh's leaves hold at most BVH_MAX_PRIMS (src/bvh.jl:32,166)
+            return jt::fail(JT_ERR_INVALID, std::string(what) + ": a leaf above BVH_MAX_PRIMS (4) primitives");
         }
     }
     for (int k = 0; k < t.nprimitives; k++)
@@ -809,6 +811,14 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                                in.material, in.shape, scene->materials[in.material].type,
                                rot_identity(fv) ? 1 : 0};
     }
+    // per device instance the first instance of its TLAS leaf (instances are numbered in TLAS
+    // leaf order, so a leaf's instances are a range)
+    std::vector<int> inst_tleaf(std::max(1, scene->ninstances), 0);
+    for (int k = 0; k < bvh->tlas.nnodes; k++) {
+        const jt_bvh_node& n = bvh->tlas.nodes[k];
+        if (n.internal) continue;
+        for (int q = 0; q < n.num; q++) inst_tleaf[inst_new[bvh->tlas.primitives[n.start + q]]] = inst_new[bvh->tlas.primitives[n.start]];
+    }
     // flat list of (device instance, record) pairs: every record of every instance's shape, in
     // instance order (JT_FLAT experiment)
     std::vector<int2> flat;
@@ -958,7 +968,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, enrm, &S.enrm)) || (st = upload(c, enrm_id, &S.enrm_id)) ||
         (st = upload(c, mats, &S.materials)) || (st = upload(c, texs, &S.textures)) || (st = upload(c, texb, &S.texb)) ||
         (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) || (st = upload(c, lhit, &S.light_hit)) || (st = upload(c, lelems, &S.light_elems)) ||
-        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)) || (st = upload(c, flat, &S.flat)))
+        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)) || (st = upload(c, flat, &S.flat)) || (st = upload(c, inst_tleaf, &S.inst_tleaf)))
         return bail(st);
     S.nflat = (int)flat.size();
     S.tlas_nnodes = (int)tlas.size();
