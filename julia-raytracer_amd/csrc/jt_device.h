@@ -172,8 +172,6 @@ struct DScene {
     int tlas_nnodes, nenvs, nlights;
     const int* inst_tleaf;  // per instance: the first instance of its TLAS leaf (the near-first
                             // orders' tie decision, jtk::tie_ok; read only at an exact-t tie)
-    const int2* flat;  // (instance, record) of every primitive record of every instance (JT_FLAT)
-    int nflat;
     int order_flip;  // jt_params.traversal: 0 the reference's child order, 7 the near child first
                      // (near and wide)
     float light_pick_pdf;  // sample_uniform_pdf(nlights) = Float32(1 / nlights) (src/sampling.jl:31)

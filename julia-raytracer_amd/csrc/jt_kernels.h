@@ -385,23 +385,35 @@ struct Trav {
 // their order. A tie with the closest hit so far therefore wins in the reference's order iff it
 // is in the same BLAS leaf (a later primitive), or in another instance of the same TLAS leaf (a
 // later instance); from an earlier BLAS leaf of the same instance, or an earlier TLAS leaf, the
-// hit so far is the reference's later one and stays. Ties are rare (2e-5 of bathroom1's queries,
-// none on cornellbox), so the decision is made only at a tie: the same leaf is known to the
-// primitive step (a triangle leaf, <= 4 primitives, is tested within one step; a quad leaf keeps
-// TIE_LEAF in nh), the same instance from the hit's instance, the same TLAS leaf from a per-
-// instance table (DScene::inst_tleaf). The reference's own order accepts every tie.
+// hit so far is the reference's later one and stays. A tie does not move tmax, so it changes no
+// box test: only which primitive the query reports. Ties are rare (2e-5 of bathroom1's queries,
+// none on cornellbox), so the primitive step only checks, per triangle, whether any lane of the
+// wave has one (a wave-uniform branch), and decides there: the same leaf from the leaf's element
+// ids (a triangle leaf, <= 4 primitives, is tested within one step) or, for quads, TIE_LEAF in
+// nh; the same instance from the hit's instance; the same TLAS leaf from a per-instance table
+// (DScene::inst_tleaf). The reference's own order accepts every tie.
 #ifndef JT_TIE
 #define JT_TIE 1
 #endif
 constexpr int TIE_LEAF = 1 << 8, NH_COUNT = 63;
-__device__ __forceinline__ bool tie_ok(const DScene& S, const Trav& T, bool same_leaf) {
+__device__ __forceinline__ bool tie_wins(const DScene& S, const Trav& T, bool same_leaf) {
     if (!JT_TIE || S.order_flip == 0 || same_leaf) return true;
     if (T.h_inst == T.cur_inst) return false;  // an earlier BLAS leaf of this instance
     return S.inst_tleaf[T.h_inst] == S.inst_tleaf[T.cur_inst];  // an earlier instance of this TLAS leaf
 }
-// a hit at t (t <= tmax already) replaces the closest hit so far
-__device__ __forceinline__ bool accept_hit(const DScene& S, const Trav& T, float t, bool same_leaf) {
-    return t < T.tmax || tie_ok(S, T, same_leaf);
+// a tie in the current triangle leaf (pair records T.prim, T.prim + 1; T.nprim triangles): is the
+// hit so far one of this leaf's triangles (element ids are unique within a shape)?
+__device__ __forceinline__ bool tri_tie_wins(const DScene& S, const Trav& T) {
+    bool same = false;
+    if (T.h_inst == T.cur_inst) {
+        const float4 a = S.prims[5 * T.prim + 4];
+        same = T.h_elem == __float_as_int(a.z) || (T.nprim > 1 && T.h_elem == __float_as_int(a.w));
+        if (T.nprim > 2) {
+            const float4 b = S.prims[5 * T.prim + 9];
+            same = same || T.h_elem == __float_as_int(b.z) || (T.nprim > 3 && T.h_elem == __float_as_int(b.w));
+        }
+    }
+    return tie_wins(S, T, same);
 }
 __device__ __forceinline__ void hit_count(Trav& T) { T.nh += (T.nh & NH_COUNT) < NH_COUNT ? 1 : 0; }
 
@@ -501,25 +513,29 @@ __device__ __forceinline__ void query_start(const DScene& S, Trav& T, v3 o, v3 d
 // the two triangles' components interleaved, 5 loads instead of 6 for two separate records).
 // k is 0 or 2.
 template <int F>
-__device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k, bool& leaf_hit) {
+__device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
     const float4* r = S.prims + 5 * (T.prim + (k >> 1));
     const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
     const PrimHit p1 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.x, r0.z, r1.x), V3(r1.z, r2.x, r2.z),
                                               V3(r3.x, r3.z, r4.x));
     const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.y, r0.w, r1.y), V3(r1.w, r2.y, r2.w),
                                               V3(r3.y, r3.w, r4.y));
-    if (tri_hit_before(p1, T.tmax) && accept_hit(S, T, p1.t, leaf_hit)) {
+    bool a1 = tri_hit_before(p1, T.tmax);
+    if (JT_TIE && __builtin_amdgcn_ballot_w64(a1 && p1.t == T.tmax))  // an exact-t tie in the wave (rare)
+        if (a1 && p1.t == T.tmax) a1 = tri_tie_wins(S, T);
+    if (a1) {
         hit_count(T);
-        leaf_hit = true;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.z);
         T.h_u = p1.u;
         T.h_v = p1.v;
         T.tmax = p1.t;
     }
-    if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax) && accept_hit(S, T, p2.t, leaf_hit)) {
+    bool a2 = T.nprim >= k + 2 && tri_hit_before(p2, T.tmax);
+    if (JT_TIE && __builtin_amdgcn_ballot_w64(a2 && p2.t == T.tmax))
+        if (a2 && p2.t == T.tmax) a2 = tri_tie_wins(S, T);
+    if (a2) {
         hit_count(T);
-        leaf_hit = true;
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.w);
         T.h_u = p2.u;
@@ -531,11 +547,10 @@ template <int COUNT, int F>
 __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cnt) {
     if (!(F & FT_QUAD) || T.cur_kind == KIND_TRI) {
         // a triangle leaf (<= 4 primitives, BVH_MAX_PRIMS, src/bvh.jl:32) is tested within this step
-        bool leaf_hit = false;
-        tri_pair<F>(S, T, 0, leaf_hit);
+        tri_pair<F>(S, T, 0);
         const bool more = T.nprim > 2;
         if (__builtin_amdgcn_ballot_w64(more)) {
-            if (more) tri_pair<F>(S, T, 2, leaf_hit);
+            if (more) tri_pair<F>(S, T, 2);
         }
         const int n = T.nprim < 4 ? T.nprim : 4;
         if (COUNT) cnt.prims += n;
@@ -547,7 +562,10 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     const float4* r = S.prims + 4 * T.prim;
     const float4 a = r[0], b = r[1], c = r[2], d = r[3];
     const PrimHit p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
-    if (p.hit && accept_hit(S, T, p.t, (T.nh & TIE_LEAF) != 0)) {
+    bool acc = p.hit;
+    if (JT_TIE && __builtin_amdgcn_ballot_w64(acc && p.t == T.tmax))
+        if (acc && p.t == T.tmax) acc = tie_wins(S, T, (T.nh & TIE_LEAF) != 0);
+    if (acc) {
         hit_count(T);
         T.nh |= TIE_LEAF;
         T.h_inst = T.cur_inst;
@@ -818,36 +836,6 @@ __device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* st
         w = (unsigned)ib.x;
     }
     wide_visit<RING, OVF, COUNT, F>(S, T, stack, pixel, cnt, w);
-}
-// JT_FLAT (experiment): a small scene's closest-hit query tests every primitive record of every
-// instance at once (uniform control, every lane of the wave together), FT_NONE scenes only
-#ifndef JT_FLAT
-#define JT_FLAT 0
-#endif
-template <int F>
-__device__ __forceinline__ void flat_query(const DScene& S, Trav& T, v3 o, v3 d) {
-    T.wo = o;
-    T.wd = d;
-    T.lo = o;
-    T.ld = d;
-    T.tmax = __builtin_inff();
-    T.nh = 0;
-    T.h_inst = -1;
-    T.h_elem = -1;
-    T.h_u = 0;
-    T.h_v = 0;
-    T.nprim = 0;
-    T.sp = 0;
-    T.nxt = W_EMPTY;
-    for (int k = 0; k < S.nflat; k++) {
-        const int2 ir = S.flat[k];
-        T.cur_inst = ir.x;
-        T.prim = ir.y;
-        T.nprim = 2;
-        bool lh = false;
-        tri_pair<F>(S, T, 0, lh);
-    }
-    T.nprim = 0;
 }
 // a node step in either traversal
 template <bool WIDE, int RING, bool OVF, int COUNT, bool NCACHE, int F>
@@ -1607,8 +1595,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
             const int pixel = item_pixel(item, P, tiles_x);
             if (!ft_none(F)) acc[12 * BLOCK] = stream_weight(P, sample);
             start_path<F>(P, pixel % P.width, pixel / P.width, pixel, sample, st);
-            if constexpr (JT_FLAT && ft_none(F) && !WIDE) flat_query<F>(S, T, st.o, st.d);
-            else query_start<WIDE>(S, T, st.o, st.d, -1, stack);
+            query_start<WIDE>(S, T, st.o, st.d, -1, stack);
             if (!WC) lds_count(1, true);
             if constexpr (item_first_pop<WIDE, F>()) {
 #pragma unroll
@@ -1799,8 +1786,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 } else {
                     if (WC) c_ray = true;
                     else lds_count(1, true);
-                    if constexpr (JT_FLAT && ft_none(F) && !WIDE) flat_query<F>(S, T, st.o, st.d);
-                    else query_start<WIDE>(S, T, st.o, st.d, -1, stack);
+                    query_start<WIDE>(S, T, st.o, st.d, -1, stack);
                 }
                 // the query's first pop (TLAS root, or the light instance and its BLAS root) here,
                 // where most of the wave's lanes take part, rather than in a sparser traversal step

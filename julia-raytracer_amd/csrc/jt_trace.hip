@@ -309,7 +309,14 @@ float exp_scale(int e) {  // 2^(e - 127), e = a normal float's biased exponent
 // (and the next larger ones until every child fits). leaf_word(k): the child word of binary leaf
 // k. Returns the root record's index, or -1 with the error set.
 int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_word, std::vector<DWide>& out) {
-    if (t.nnodes <= 0) return jt::fail(JT_ERR_INVALID, "wide traversal: empty BVH"), -1;
+    if (t.nnodes <= 0 || (!t.nodes[0].internal && t.nodes[0].num <= 0)) {
+        // an empty tree (make_bvh of no boxes is one leaf without primitives, src/bvh.jl:138-183):
+        // one record without children, so a query visits it and finds nothing
+        DWide w{};
+        w.r3 = make_uint4(W_EMPTY, W_EMPTY, W_EMPTY, W_EMPTY);
+        out.push_back(w);
+        return (int)out.size() - 1;
+    }
     std::vector<int> q{0}, rec{(int)out.size()};
     out.emplace_back();
     for (size_t h = 0; h < q.size(); h++) {
@@ -635,7 +642,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     // the record (pair / quad) where each binary BLAS leaf's primitives start: the wide records'
     // leaf words (JT_TRAVERSAL_WIDE)
     std::vector<std::vector<int>> leaf_rec(scene->nshapes);
-    std::vector<int> shape_nrec(scene->nshapes, 0);  // pair / quad records of each shape
     for (int s = 0; s < scene->nshapes; s++) {
         const jt_shape& sh = scene->shapes[s];
         const jt_bvh_tree& t = bvh->blas[s];
@@ -731,7 +737,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                     pairs++;
                 }
             }
-            shape_nrec[s] = pairs;
             continue;
         }
         for (int k = 0; k < t.nnodes; k++) {
@@ -739,7 +744,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
             blas.push_back(pack_node(n, n.internal ? d.blas_root + n.start : d.prim_base + n.start));
             if (!n.internal) leaf_rec[s][k] = d.prim_base + n.start;
         }
-        shape_nrec[s] = t.nprimitives;
         // quad records in BVH leaf order (the reference reads positions through
         // bvh.primitives[i]; the records hold the same floats, pre-gathered)
         for (int k = 0; k < t.nprimitives; k++) {
@@ -819,11 +823,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         if (n.internal) continue;
         for (int q = 0; q < n.num; q++) inst_tleaf[inst_new[bvh->tlas.primitives[n.start + q]]] = inst_new[bvh->tlas.primitives[n.start]];
     }
-    // flat list of (device instance, record) pairs: every record of every instance's shape, in
-    // instance order (JT_FLAT experiment)
-    std::vector<int2> flat;
-    for (int k = 0; k < scene->ninstances; k++)
-        for (int r = 0; r < shape_nrec[iblas[k].w]; r++) flat.push_back(make_int2(k, shapes[iblas[k].w].prim_base + r));
     std::vector<DMaterial> mats(scene->nmaterials);
     for (int k = 0; k < scene->nmaterials; k++) {
         const jt_material& m = scene->materials[k];
@@ -968,9 +967,8 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, enrm, &S.enrm)) || (st = upload(c, enrm_id, &S.enrm_id)) ||
         (st = upload(c, mats, &S.materials)) || (st = upload(c, texs, &S.textures)) || (st = upload(c, texb, &S.texb)) ||
         (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) || (st = upload(c, lhit, &S.light_hit)) || (st = upload(c, lelems, &S.light_elems)) ||
-        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)) || (st = upload(c, flat, &S.flat)) || (st = upload(c, inst_tleaf, &S.inst_tleaf)))
+        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)) || (st = upload(c, inst_tleaf, &S.inst_tleaf)))
         return bail(st);
-    S.nflat = (int)flat.size();
     S.tlas_nnodes = (int)tlas.size();
     S.tlas_wnodes = tlas_wnodes;
     S.order_flip = params->traversal == JT_TRAVERSAL_REFERENCE ? 0 : 7;  // near and wide: near child first

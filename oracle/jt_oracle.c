@@ -562,6 +562,11 @@ static int w_build(const jt_bvh_tree* b, int node, wtree_t* t) {
     int r = w_add(t);
     if (r < 0) return -1;
     const jt_bvh_node* N = &b->nodes[node];
+    if (!N->internal && N->num <= 0) { /* an empty tree (no boxes): a record without children */
+        memset(&t->r[r], 0, sizeof(wrec_t));
+        for (int k = 0; k < 4; k++) t->r[r].child[k] = t->r[r].rec[k] = -1;
+        return r;
+    }
     int slot[4] = {-1, -1, -1, -1}, a1 = 0, a2 = 0;
     if (!N->internal) {
         slot[0] = node;

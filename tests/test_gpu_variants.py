@@ -18,10 +18,10 @@ from conftest import compare_images, make_params
 pytestmark = pytest.mark.gpu
 
 
-def _parity(abi, lib, oracle, scene, label, sampler=1, spp=6, res=96):
+def _parity(abi, lib, oracle, scene, label, sampler=1, spp=6, res=96, traversal="near"):
     from jtrace import trace
     sa = abi.SceneABI(scene)
-    p = make_params(abi, resolution=res, samples=spp, sampler=sampler)
+    p = make_params(abi, resolution=res, samples=spp, sampler=sampler, traversal=traversal)
     bvh = trace.make_scene_bvh(sa, False, lib)
     lights = trace.make_trace_lights(sa, lib)
     st = trace.make_trace_state(sa, bvh, lights, p, lib)
@@ -78,3 +78,22 @@ def test_vertex_colors_parity(gpu, abi, lib, oracle, cornell, sampler):
         s.colors = col
     g, o = _parity(abi, lib, oracle, sc, f"vcolor/{sampler}", sampler=sampler)
     assert ",255," in g[5]  # FT_ATTR | FT_OPAC: the general kernel
+
+
+@pytest.mark.parametrize("order", ["near", "wide", "reference"])
+def test_environment_only_scene(gpu, abi, lib, oracle, order):
+    """A scene without instances (features2's environment and camera only): make_bvh of no
+    boxes is one leaf without primitives (src/bvh.jl:138-183), every query misses, every path
+    sees the environment. Every traversal, the wide one included (an empty tree is one record
+    without children), against the oracle."""
+    import warnings
+    from conftest import ROOT
+    from jtrace import sceneio
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        sc = sceneio.load_scene(str(ROOT / "assets" / "scenes" / "features2" / "features2.json"), missing="drop")
+    sc.instances = []
+    g, o = _parity(abi, lib, oracle, sc, f"env-only/{order}", traversal=order)
+    assert f"traversal={order}" in g[5]
+    assert g[4]["rays"] > 0 and g[4]["shades"] == 0
+    assert float(g[0][..., 3].min()) == 1.0  # the environment is visible everywhere
