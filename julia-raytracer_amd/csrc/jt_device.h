@@ -170,8 +170,6 @@ struct DScene {
     const float* srgb_lut;  // srgb_to_rgb(byte_to_float(b)), 256 entries (src/color.jl:12-23)
     const float* byte_lut;  // byte_to_float(b)
     int tlas_nnodes, nenvs, nlights;
-    const int* inst_tleaf;  // per instance: the first instance of its TLAS leaf (the near-first
-                            // orders' tie decision, jtk::tie_ok; read only at an exact-t tie)
     int order_flip;  // jt_params.traversal: 0 the reference's child order, 7 the near child first
                      // (near and wide)
     float light_pick_pdf;  // sample_uniform_pdf(nlights) = Float32(1 / nlights) (src/sampling.jl:31)

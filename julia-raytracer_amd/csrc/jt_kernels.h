@@ -373,49 +373,30 @@ struct Trav {
     int h_inst, h_elem;  // closest hit so far (instance -1: none); its distance is tmax
     float h_u, h_v;
     int nh;              // bits 0-5: hits accepted so far (every tmax change), saturating at 63;
-                         // bit 8 (quad scenes): the closest hit so far is in the current leaf (TIE_LEAF)
+                         // TIE_SEEN, REF_RERUN (the tie rule below)
     unsigned nxt;        // wide traversal: the child word visited by the next node step (W_EMPTY: pop)
 };
 
 // Exact-t ties in the near-first orders (JT_TRAVERSAL_NEAR / WIDE). The reference accepts a hit
 // at t == tmax (src/geometry.jl:226, only t > tmax rejects), so among equal-t hits the one it
-// tests LAST wins. The near-first orders visit every internal node's children in the opposite
-// order (at every level of both trees), so they reach the leaves of a tree in exactly the
-// reverse of the reference's sequence, while a leaf's primitives and a TLAS leaf's instances keep
-// their order. A tie with the closest hit so far therefore wins in the reference's order iff it
-// is in the same BLAS leaf (a later primitive), or in another instance of the same TLAS leaf (a
-// later instance); from an earlier BLAS leaf of the same instance, or an earlier TLAS leaf, the
-// hit so far is the reference's later one and stays. A tie does not move tmax, so it changes no
-// box test: only which primitive the query reports. Ties are rare (2e-5 of bathroom1's queries,
-// none on cornellbox), so the primitive step only checks, per triangle, whether any lane of the
-// wave has one (a wave-uniform branch), and decides there: the same leaf from the leaf's element
-// ids (a triangle leaf, <= 4 primitives, is tested within one step) or, for quads, TIE_LEAF in
-// nh; the same instance from the hit's instance; the same TLAS leaf from a per-instance table
-// (DScene::inst_tleaf). The reference's own order accepts every tie.
-#ifndef JT_TIE
-#define JT_TIE 1
+// tests LAST wins, and which one that is depends on its child order (src/bvh.jl:331-341). A
+// near-first query that accepts a hit at exactly its current tmax (TIE_SEEN) is therefore run
+// again in the reference's child order (REF_RERUN: the same records, the children visited far
+// first; with the wide records that is the binary far-first leaf sequence) and reports that
+// query's hit instead: the reference's own tie resolution. Ties are rare (2e-5 of bathroom1's
+// queries, none on cornellbox), so the hot path only records them (at an accepted hit), and the
+// re-run runs where the query's hit is consumed (rerun_tie). A re-run is the same query: it is
+// not counted as a ray or light query again; its node and primitive work is counted (COUNT=1).
+#ifndef JT_TIE_RERUN
+#define JT_TIE_RERUN 1  // 0: ties resolve in the near-first order's own sequence (A/B runs only)
 #endif
-constexpr int TIE_LEAF = 1 << 8, NH_COUNT = 63;
-__device__ __forceinline__ bool tie_wins(const DScene& S, const Trav& T, bool same_leaf) {
-    if (!JT_TIE || S.order_flip == 0 || same_leaf) return true;
-    if (T.h_inst == T.cur_inst) return false;  // an earlier BLAS leaf of this instance
-    return S.inst_tleaf[T.h_inst] == S.inst_tleaf[T.cur_inst];  // an earlier instance of this TLAS leaf
+constexpr int TIE_SEEN = 1 << 8, REF_RERUN = 1 << 9, NH_COUNT = 63;
+// the child-order flip of the lane's current query: near-first, unless it is a tie's re-run
+__device__ __forceinline__ int query_flip(const DScene& S, const Trav& T) { return (T.nh & REF_RERUN) ? 0 : S.order_flip; }
+// a hit accepted at t (t <= tmax): count it (child pre-test snapshots) and note an exact-t tie
+__device__ __forceinline__ void hit_count(Trav& T, float t) {
+    T.nh = (T.nh + ((T.nh & NH_COUNT) < NH_COUNT ? 1 : 0)) | (JT_TIE_RERUN && t == T.tmax ? TIE_SEEN : 0);
 }
-// a tie in the current triangle leaf (pair records T.prim, T.prim + 1; T.nprim triangles): is the
-// hit so far one of this leaf's triangles (element ids are unique within a shape)?
-__device__ __forceinline__ bool tri_tie_wins(const DScene& S, const Trav& T) {
-    bool same = false;
-    if (T.h_inst == T.cur_inst) {
-        const float4 a = S.prims[5 * T.prim + 4];
-        same = T.h_elem == __float_as_int(a.z) || (T.nprim > 1 && T.h_elem == __float_as_int(a.w));
-        if (T.nprim > 2) {
-            const float4 b = S.prims[5 * T.prim + 9];
-            same = same || T.h_elem == __float_as_int(b.z) || (T.nprim > 3 && T.h_elem == __float_as_int(b.w));
-        }
-    }
-    return tie_wins(S, T, same);
-}
-__device__ __forceinline__ void hit_count(Trav& T) { T.nh += (T.nh & NH_COUNT) < NH_COUNT ? 1 : 0; }
 
 __device__ __forceinline__ int neg_mask(v3 d, int flip) {
     return ((d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0)) ^ flip;
@@ -425,7 +406,7 @@ __device__ __forceinline__ void world_ray(const DScene& S, Trav& T) {
     T.lo = T.wo;
     T.ld = T.wd;
     T.ldinv = T.wdinv;
-    T.negmask = neg_mask(T.wd, S.order_flip);
+    T.negmask = neg_mask(T.wd, query_flip(S, T));
     T.inst_space = 0;
 }
 
@@ -446,7 +427,7 @@ __device__ __forceinline__ bool query_done(const Trav& T) {
     return (T.sp | T.nprim) == 0 && (!WIDE || T.nxt == W_EMPTY);
 }
 
-__device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d, unsigned root, int* stack) {
+__device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d, unsigned root, int* stack, int rerun = 0) {
     T.wo = o;
     T.wd = d;
     T.wdinv = V3(jl_rcp(d.x), jl_rcp(d.y), jl_rcp(d.z));  // ray_dinv (src/bvh.jl:322), no guard
@@ -454,7 +435,7 @@ __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d
     T.ld = d;
     T.ldinv = T.wdinv;
     T.tmax = __builtin_inff();
-    T.nh = 0;
+    T.nh = rerun;
     T.h_inst = -1;
     T.h_elem = -1;
     T.h_u = 0;
@@ -464,7 +445,7 @@ __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d
     T.cur_inst = -1;
     T.cur_kind = KIND_TRI;
     T.inst_space = 0;
-    T.negmask = neg_mask(d, S.order_flip);
+    T.negmask = neg_mask(d, rerun ? 0 : S.order_flip);
     stack[0] = (int)root;
     T.sp = 1;
     T.low = 0;
@@ -472,7 +453,7 @@ __device__ __forceinline__ void query_begin(const DScene& S, Trav& T, v3 o, v3 d
 }
 // query_begin of the wide traversal: the root is the first node step's child word (the TLAS
 // root record, or an instance leaf of one instance for intersect_instance_bvh); the stack is empty
-__device__ __forceinline__ void query_begin_wide(const DScene& S, Trav& T, v3 o, v3 d, unsigned root_word) {
+__device__ __forceinline__ void query_begin_wide(const DScene& S, Trav& T, v3 o, v3 d, unsigned root_word, int rerun = 0) {
     T.wo = o;
     T.wd = d;
     T.wdinv = V3(jl_rcp(d.x), jl_rcp(d.y), jl_rcp(d.z));  // ray_dinv (src/bvh.jl:322), no guard
@@ -480,7 +461,7 @@ __device__ __forceinline__ void query_begin_wide(const DScene& S, Trav& T, v3 o,
     T.ld = d;
     T.ldinv = T.wdinv;
     T.tmax = __builtin_inff();
-    T.nh = 0;
+    T.nh = rerun;
     T.h_inst = -1;
     T.h_elem = -1;
     T.h_u = 0;
@@ -490,7 +471,7 @@ __device__ __forceinline__ void query_begin_wide(const DScene& S, Trav& T, v3 o,
     T.cur_inst = -1;
     T.cur_kind = KIND_TRI;
     T.inst_space = 0;
-    T.negmask = neg_mask(d, S.order_flip);
+    T.negmask = neg_mask(d, rerun ? 0 : S.order_flip);
     T.sp = 0;
     T.low = 0;
     T.nxt = root_word;
@@ -500,9 +481,18 @@ __device__ __forceinline__ unsigned wroot_instance(int inst) { return W_LEAF | W
 // query_begin for either traversal: a closest-hit scene query, or (inst >= 0) the
 // intersect_instance_bvh of sample_lights_pdf
 template <bool WIDE>
-__device__ __forceinline__ void query_start(const DScene& S, Trav& T, v3 o, v3 d, int inst, int* stack) {
-    if (WIDE) query_begin_wide(S, T, o, d, inst < 0 ? WROOT_SCENE : wroot_instance(inst));
-    else query_begin(S, T, o, d, inst < 0 ? ((T_TLAS << 30) | SNAP_NONE) : ((T_INST << 30) | SNAP_NONE | (unsigned)inst), stack);
+__device__ __forceinline__ void query_start(const DScene& S, Trav& T, v3 o, v3 d, int inst, int* stack, int rerun = 0) {
+    if (WIDE) query_begin_wide(S, T, o, d, inst < 0 ? WROOT_SCENE : wroot_instance(inst), rerun);
+    else query_begin(S, T, o, d, inst < 0 ? ((T_TLAS << 30) | SNAP_NONE) : ((T_INST << 30) | SNAP_NONE | (unsigned)inst), stack, rerun);
+}
+// a finished near-first query that saw an exact-t tie: run it again in the reference's child order
+// (the same world ray; inst >= 0: the intersect_instance_bvh of that instance). Returns whether
+// the lane re-runs (its query is then not done).
+template <bool WIDE>
+__device__ __forceinline__ bool rerun_tie(const DScene& S, Trav& T, int inst, int* stack) {
+    if (!JT_TIE_RERUN || (T.nh & (TIE_SEEN | REF_RERUN)) != TIE_SEEN || S.order_flip == 0) return false;
+    query_start<WIDE>(S, T, T.wo, T.wd, inst, stack, REF_RERUN);
+    return true;
 }
 
 // The current BLAS leaf's next primitive(s), in order (src/bvh.jl:444-484). Triangles go in
@@ -520,22 +510,16 @@ __device__ __forceinline__ void tri_pair(const DScene& S, Trav& T, int k) {
                                               V3(r3.x, r3.z, r4.x));
     const PrimHit p2 = intersect_triangle_pre(T.lo, T.ld, ray_eps, V3(r0.y, r0.w, r1.y), V3(r1.w, r2.y, r2.w),
                                               V3(r3.y, r3.w, r4.y));
-    bool a1 = tri_hit_before(p1, T.tmax);
-    if (JT_TIE && __builtin_amdgcn_ballot_w64(a1 && p1.t == T.tmax))  // an exact-t tie in the wave (rare)
-        if (a1 && p1.t == T.tmax) a1 = tri_tie_wins(S, T);
-    if (a1) {
-        hit_count(T);
+    if (tri_hit_before(p1, T.tmax)) {
+        hit_count(T, p1.t);
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.z);
         T.h_u = p1.u;
         T.h_v = p1.v;
         T.tmax = p1.t;
     }
-    bool a2 = T.nprim >= k + 2 && tri_hit_before(p2, T.tmax);
-    if (JT_TIE && __builtin_amdgcn_ballot_w64(a2 && p2.t == T.tmax))
-        if (a2 && p2.t == T.tmax) a2 = tri_tie_wins(S, T);
-    if (a2) {
-        hit_count(T);
+    if (T.nprim >= k + 2 && tri_hit_before(p2, T.tmax)) {
+        hit_count(T, p2.t);
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(r4.w);
         T.h_u = p2.u;
@@ -562,12 +546,8 @@ __device__ __forceinline__ void prim_step(const DScene& S, Trav& T, Counters& cn
     const float4* r = S.prims + 4 * T.prim;
     const float4 a = r[0], b = r[1], c = r[2], d = r[3];
     const PrimHit p = intersect_quad(T.lo, T.ld, ray_eps, T.tmax, xyz(a), xyz(b), xyz(c), xyz(d), d.w != 0.0f);
-    bool acc = p.hit;
-    if (JT_TIE && __builtin_amdgcn_ballot_w64(acc && p.t == T.tmax))
-        if (acc && p.t == T.tmax) acc = tie_wins(S, T, (T.nh & TIE_LEAF) != 0);
-    if (acc) {
-        hit_count(T);
-        T.nh |= TIE_LEAF;
+    if (p.hit) {
+        hit_count(T, p.t);
         T.h_inst = T.cur_inst;
         T.h_elem = __float_as_int(a.w);
         T.h_u = p.u;
@@ -632,7 +612,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
             T.lo = transform_point(inv, T.wo);
             T.ld = transform_vector(inv, T.wd);
             T.ldinv = V3(jl_rcp(T.ld.x), jl_rcp(T.ld.y), jl_rcp(T.ld.z));
-            T.negmask = neg_mask(T.ld, S.order_flip);
+            T.negmask = neg_mask(T.ld, query_flip(S, T));
             T.inst_space = 1;
         }
         T.cur_inst = (int)idx;
@@ -703,7 +683,7 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
     } else {  // BLAS leaf: its primitives are tested next, in order, before any other pop
         T.prim = start;
         T.nprim = num;
-        if (F & FT_QUAD) T.nh &= ~TIE_LEAF;
+
     }
 }
 
@@ -754,7 +734,7 @@ __device__ __forceinline__ void wide_take(Trav& T, unsigned w) {
     const bool leaf = (w & (W_LEAF | W_INST)) == W_LEAF;  // a BLAS leaf: its primitives are tested next
     T.prim = leaf ? (int)(w & W_START) : T.prim;
     T.nprim = leaf ? (int)((w >> 28) & 3u) + 1 : T.nprim;
-    if (F & FT_QUAD) T.nh = leaf ? T.nh & ~TIE_LEAF : T.nh;
+
     T.nxt = leaf ? T.nxt : w;  // a record, or a TLAS leaf (its first instance is visited by the next step)
 }
 // one record visit: the up-to-four child boxes against the current ray and tmax; the first passing
@@ -828,7 +808,7 @@ __device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* st
             T.lo = transform_point(inv, T.wo);
             T.ld = transform_vector(inv, T.wd);
             T.ldinv = V3(jl_rcp(T.ld.x), jl_rcp(T.ld.y), jl_rcp(T.ld.z));
-            T.negmask = neg_mask(T.ld, S.order_flip);
+            T.negmask = neg_mask(T.ld, query_flip(S, T));
             T.inst_space = 1;
         }
         T.cur_inst = (int)inst;
@@ -1116,9 +1096,14 @@ __device__ __forceinline__ bool light_chain(const DScene& S, const DParams& P, P
                                             Counters& cnt, CountLq count_lq) {
     do {
         count_lq();
-        query_start<WIDE>(S, T, st.o, st.d, S.lights[st.li].instance, stack);
+        const int inst = S.lights[st.li].instance;
+        query_start<WIDE>(S, T, st.o, st.d, inst, stack);
         node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);  // instance + its one-leaf root
         while (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+        if (rerun_tie<WIDE>(S, T, inst, stack)) {  // an exact-t tie: the reference's order decides
+            node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
+            while (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+        }
         if (light_hit<F>(S, P, st, query_hit(T))) return true;
     } while (st.phase == PH_LIGHT);
     return false;
@@ -1631,7 +1616,9 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 const int nl = lane_count(__builtin_amdgcn_ballot_w64(wantl));
                 if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
                     bool c_lq = false, c_ray = false;
-                    if (wantl) {
+                    if (wantl && rerun_tie<WIDE>(S, T, S.lights[st.li].instance, stack)) {
+                        // an exact-t tie: the query runs again in the reference's order
+                    } else if (wantl) {
                         if (light_hit<F>(S, P, st, query_hit(T))) {
                             st.phase = PH_FINISH;
                         } else if (st.phase == PH_LIGHT) {
@@ -1704,13 +1691,20 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
         }
         unsigned long long ts3 = ts2, ts4 = ts2;
 #endif
-        // ---- shading phase: every waiting lane consumes its hit and issues its next query
+        // ---- shading phase: every waiting lane consumes its hit and issues its next query; a
+        // near-first query that saw an exact-t tie first runs again in the reference's order
+        constexpr bool LINL = (F & (FT_LINL | FT_NOIL)) != 0;
+        {
+            const bool tie = query_done<WIDE>(T) && (T.nh & (TIE_SEEN | REF_RERUN)) == TIE_SEEN &&
+                             !(LSTEP && st.phase == PH_FINISH);
+            if (S.order_flip && __builtin_amdgcn_ballot_w64(tie))
+                if (tie) rerun_tie<WIDE>(S, T, SAMPLER == 1 && !LINL && st.phase == PH_LIGHT ? S.lights[st.li].instance : -1, stack);
+        }
         bool c_path = false, c_lq = false, c_ray = false;
         unsigned n_inl = 0;
         if (query_done<WIDE>(T)) {
             bool alive = true;
             // no light query ever leaves the shading phase (FT_LINL), or none exists (FT_NOIL)
-            constexpr bool LINL = (F & (FT_LINL | FT_NOIL)) != 0;
             const bool light = SAMPLER == 1 && !LINL && st.phase == PH_LIGHT;
             bool done;
             if (LSTEP && st.phase == PH_FINISH) done = true;

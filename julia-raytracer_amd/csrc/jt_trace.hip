@@ -815,14 +815,6 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                                in.material, in.shape, scene->materials[in.material].type,
                                rot_identity(fv) ? 1 : 0};
     }
-    // per device instance the first instance of its TLAS leaf (instances are numbered in TLAS
-    // leaf order, so a leaf's instances are a range)
-    std::vector<int> inst_tleaf(std::max(1, scene->ninstances), 0);
-    for (int k = 0; k < bvh->tlas.nnodes; k++) {
-        const jt_bvh_node& n = bvh->tlas.nodes[k];
-        if (n.internal) continue;
-        for (int q = 0; q < n.num; q++) inst_tleaf[inst_new[bvh->tlas.primitives[n.start + q]]] = inst_new[bvh->tlas.primitives[n.start]];
-    }
     std::vector<DMaterial> mats(scene->nmaterials);
     for (int k = 0; k < scene->nmaterials; k++) {
         const jt_material& m = scene->materials[k];
@@ -967,7 +959,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         (st = upload(c, enrm, &S.enrm)) || (st = upload(c, enrm_id, &S.enrm_id)) ||
         (st = upload(c, mats, &S.materials)) || (st = upload(c, texs, &S.textures)) || (st = upload(c, texb, &S.texb)) ||
         (st = upload(c, texf, &S.texf)) || (st = upload(c, envs, &S.envs)) || (st = upload(c, dl, &S.lights)) || (st = upload(c, lhit, &S.light_hit)) || (st = upload(c, lelems, &S.light_elems)) ||
-        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)) || (st = upload(c, inst_tleaf, &S.inst_tleaf)))
+        (st = upload(c, cdf, &S.cdf)) || (st = upload(c, guide_t, &S.guide_t)) || (st = upload(c, guide_a, &S.guide_a)) || (st = upload(c, alias, &S.alias)) || (st = upload(c, srgb, &S.srgb_lut)) || (st = upload(c, bytes, &S.byte_lut)))
         return bail(st);
     S.tlas_nnodes = (int)tlas.size();
     S.tlas_wnodes = tlas_wnodes;

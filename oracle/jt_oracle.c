@@ -354,6 +354,7 @@ typedef struct {
     const struct ctx_s* alt;
     uint64_t diag[10];
     int path_diff;
+    int tie;  /* the current near-first query accepted a hit at exactly its tmax */
 } scratch_t;
 
 static inline v3 pos3(const jt_shape* s, int32_t v) {
@@ -373,21 +374,15 @@ typedef struct { int instance, element; v2 uv; float distance; int hit; } scene_
 
 /* Exact-t ties in the near-first orders (the build's JT_TRAVERSAL_NEAR / WIDE, include/jtrace.h).
  * The reference accepts a hit at t == tmax (src/geometry.jl:226), so among equal-t hits the one
- * it tests last wins. The near-first orders visit every internal node's children in the opposite
- * order, so they reach a tree's leaves in the reverse of the reference's sequence, while a leaf's
- * primitives and a TLAS leaf's instances keep their order: an equal-t hit replaces the hit so far
- * iff it is in the same BLAS leaf, or in a later instance of the same TLAS leaf (`outer_ok`). The
- * reference's own order accepts every tie. */
-static inline int near_order(const ctx_t* c) { return c->params->traversal != JT_TRAVERSAL_REFERENCE; }
-static inline int take_hit(const ctx_t* c, const prim_isec* p, float tmax, int in_leaf, int in_inst, int outer_ok) {
-    return p->hit && (p->distance < tmax || !near_order(c) || in_leaf || (!in_inst && outer_ok));
-}
+ * it tests last wins, which depends on its child order. A near-first query that accepts a hit at
+ * exactly its current tmax (sc->tie) is run again in the reference's child order (flip 0: the same
+ * records visited far child first) and reports that query's hit: the reference's own resolution.
+ * `flip` below: 1 visits the near child first (the build's extension), 0 the reference's order. */
+static inline void note_tie(scratch_t* sc, float t, float tmax) { if (t == tmax) sc->tie = 1; }
 
-/* intersect_shape_bvh (src/bvh.jl:373-491), find_any = false; outer_ok: the ray's tmax is a hit
- * of an earlier instance of the TLAS leaf being visited (ties with it are won, see take_hit) */
-static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, scratch_t* sc, int outer_ok) {
+/* intersect_shape_bvh (src/bvh.jl:373-491), find_any = false */
+static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, scratch_t* sc, int flip) {
     shape_isec isec = {-1, {0, 0}, 0, 0};
-    int in_inst = 0, in_leaf;
     const jt_bvh_tree* bvh = &c->bvh->blas[shape_id];
     const jt_shape* shape = &c->scene->shapes[shape_id];
     if (bvh->nnodes == 0) return isec;
@@ -396,7 +391,6 @@ static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, sc
     stack[node_cur++] = 0;
     v3 dinv = V3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
     /* ray_dsign; JT_TRAVERSAL_NEAR (build extension, include/jtrace.h) inverts the push order */
-    const int flip = c->params->traversal == JT_TRAVERSAL_NEAR;
     int dsign[3] = {(ray.d.x < 0) ^ flip, (ray.d.y < 0) ^ flip, (ray.d.z < 0) ^ flip};
     while (node_cur != 0) {
         const jt_bvh_node* node = &bvh->nodes[stack[--node_cur]];
@@ -412,14 +406,13 @@ static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, sc
                 stack[node_cur++] = node->start;
             }
         } else if (shape->ntriangles > 0) {
-            in_leaf = 0;
             for (int i = node->start; i < node->start + node->num; i++) {
                 int e = bvh->primitives[i];
                 const int32_t* t = &shape->triangles[3 * e];
                 sc->cnt.prims++;
                 prim_isec p = intersect_triangle(&ray, pos3(shape, t[0]), pos3(shape, t[1]), pos3(shape, t[2]));
-                if (!take_hit(c, &p, ray.tmax, in_leaf, in_inst, outer_ok)) continue;
-                in_leaf = in_inst = 1;
+                if (!p.hit) continue;
+                note_tie(sc, p.distance, ray.tmax);
                 isec.element = e;
                 isec.uv = p.uv;
                 isec.distance = p.distance;
@@ -427,15 +420,14 @@ static shape_isec intersect_shape_bvh(const ctx_t* c, int shape_id, ray3 ray, sc
                 ray.tmax = p.distance;
             }
         } else if (shape->nquads > 0) {
-            in_leaf = 0;
             for (int i = node->start; i < node->start + node->num; i++) {
                 int e = bvh->primitives[i];
                 const int32_t* q = &shape->quads[4 * e];
                 sc->cnt.prims++;
                 prim_isec p = intersect_quad(&ray, pos3(shape, q[0]), pos3(shape, q[1]), pos3(shape, q[2]),
                                              pos3(shape, q[3]));
-                if (!take_hit(c, &p, ray.tmax, in_leaf, in_inst, outer_ok)) continue;
-                in_leaf = in_inst = 1;
+                if (!p.hit) continue;
+                note_tie(sc, p.distance, ray.tmax);
                 isec.element = e;
                 isec.uv = p.uv;
                 isec.distance = p.distance;
@@ -454,17 +446,15 @@ static inline ray3 transform_ray(const fr3* f, const ray3* r) {
 }
 
 /* intersect_scene_bvh (src/bvh.jl:306-371), find_any = false */
-static scene_isec intersect_scene_bvh(const ctx_t* c, ray3 ray, scratch_t* sc) {
+static scene_isec intersect_scene_bvh(const ctx_t* c, ray3 ray, scratch_t* sc, int flip) {
     scene_isec isec = {-1, -1, {0, 0}, 0, 0};
     const jt_bvh_tree* bvh = &c->bvh->tlas;
-    sc->cnt.rays++;
     if (bvh->nnodes == 0) return isec;
     int32_t* stack = sc->stack;
     int node_cur = 0;
     stack[node_cur++] = 0;
     v3 dinv = V3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
     /* ray_dsign; JT_TRAVERSAL_NEAR (build extension, include/jtrace.h) inverts the push order */
-    const int flip = c->params->traversal == JT_TRAVERSAL_NEAR;
     int dsign[3] = {(ray.d.x < 0) ^ flip, (ray.d.y < 0) ^ flip, (ray.d.z < 0) ^ flip};
     while (node_cur != 0) {
         const jt_bvh_node* node = &bvh->nodes[stack[--node_cur]];
@@ -480,15 +470,13 @@ static scene_isec intersect_scene_bvh(const ctx_t* c, ray3 ray, scratch_t* sc) {
                 stack[node_cur++] = node->start;
             }
         } else {
-            int in_tleaf = 0;  /* the hit so far is from an earlier instance of this TLAS leaf */
             for (int i = node->start; i < node->start + node->num; i++) {
                 int inst_id = bvh->primitives[i];
                 const jt_instance* inst = &c->scene->instances[inst_id];
                 sc->cnt.instances++;
                 ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], &ray);
-                shape_isec s = intersect_shape_bvh(c, inst->shape, inv_ray, sc, in_tleaf);
+                shape_isec s = intersect_shape_bvh(c, inst->shape, inv_ray, sc, flip);
                 if (!s.hit) continue;
-                in_tleaf = 1;
                 isec.instance = inst_id;
                 isec.element = s.element;
                 isec.uv = s.uv;
@@ -502,13 +490,12 @@ static scene_isec intersect_scene_bvh(const ctx_t* c, ray3 ray, scratch_t* sc) {
 }
 
 /* intersect_instance_bvh (src/bvh.jl:493-520) */
-static scene_isec intersect_instance_bvh(const ctx_t* c, int inst_id, ray3 ray, scratch_t* sc) {
+static scene_isec intersect_instance_bvh(const ctx_t* c, int inst_id, ray3 ray, scratch_t* sc, int flip) {
     scene_isec isec = {-1, -1, {0, 0}, 0, 0};
     const jt_instance* inst = &c->scene->instances[inst_id];
-    sc->cnt.light_queries++;
     sc->cnt.instances++;
     ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], &ray);
-    shape_isec s = intersect_shape_bvh(c, inst->shape, inv_ray, sc, 0);
+    shape_isec s = intersect_shape_bvh(c, inst->shape, inv_ray, sc, flip);
     if (!s.hit) return isec;
     isec.instance = inst_id;
     isec.element = s.element;
@@ -638,7 +625,7 @@ static void w_test(const wrec_t* w, const ray3* ray, v3 dinv, int* hit) {
     }
 }
 static void w_shape(const ctx_t* c, int shape_id, int r, ray3* ray, v3 dinv, const int* dsign, shape_isec* isec,
-                    scratch_t* sc, int outer_ok, int* in_inst) {
+                    scratch_t* sc) {
     const jt_bvh_tree* bvh = &c->bvh->blas[shape_id];
     const jt_shape* shape = &c->scene->shapes[shape_id];
     const wrec_t* w = &c->wblas[shape_id].r[r];
@@ -651,10 +638,9 @@ static void w_shape(const ctx_t* c, int shape_id, int r, ray3* ray, v3 dinv, con
         if (!hit[k]) continue;
         const jt_bvh_node* node = &bvh->nodes[w->child[k]];
         if (node->internal) {
-            w_shape(c, shape_id, w->rec[k], ray, dinv, dsign, isec, sc, outer_ok, in_inst);
+            w_shape(c, shape_id, w->rec[k], ray, dinv, dsign, isec, sc);
             continue;
         }
-        int in_leaf = 0;
         for (int i = node->start; i < node->start + node->num; i++) {
             int e = bvh->primitives[i];
             prim_isec p;
@@ -666,8 +652,8 @@ static void w_shape(const ctx_t* c, int shape_id, int r, ray3* ray, v3 dinv, con
                 const int32_t* q4 = &shape->quads[4 * e];
                 p = intersect_quad(ray, pos3(shape, q4[0]), pos3(shape, q4[1]), pos3(shape, q4[2]), pos3(shape, q4[3]));
             }
-            if (!take_hit(c, &p, ray->tmax, in_leaf, *in_inst, outer_ok)) continue;
-            in_leaf = *in_inst = 1;
+            if (!p.hit) continue;
+            note_tie(sc, p.distance, ray->tmax);
             isec->element = e;
             isec->uv = p.uv;
             isec->distance = p.distance;
@@ -677,15 +663,15 @@ static void w_shape(const ctx_t* c, int shape_id, int r, ray3* ray, v3 dinv, con
     }
 }
 /* intersect_shape_bvh on the wide records */
-static shape_isec intersect_shape_wide(const ctx_t* c, int shape_id, ray3 ray, scratch_t* sc, int outer_ok) {
+static shape_isec intersect_shape_wide(const ctx_t* c, int shape_id, ray3 ray, scratch_t* sc, int flip) {
     shape_isec isec = {-1, {0, 0}, 0, 0};
     v3 dinv = V3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
-    int dsign[3] = {(ray.d.x < 0) ^ 1, (ray.d.y < 0) ^ 1, (ray.d.z < 0) ^ 1};
-    int in_inst = 0;
-    w_shape(c, shape_id, 0, &ray, dinv, dsign, &isec, sc, outer_ok, &in_inst);
+    int dsign[3] = {(ray.d.x < 0) ^ flip, (ray.d.y < 0) ^ flip, (ray.d.z < 0) ^ flip};
+    w_shape(c, shape_id, 0, &ray, dinv, dsign, &isec, sc);
     return isec;
 }
-static void w_scene(const ctx_t* c, int r, ray3* ray, v3 dinv, const int* dsign, scene_isec* isec, scratch_t* sc) {
+static void w_scene(const ctx_t* c, int r, ray3* ray, v3 dinv, const int* dsign, scene_isec* isec, scratch_t* sc,
+                    int flip) {
     const jt_bvh_tree* bvh = &c->bvh->tlas;
     const wrec_t* w = &c->wtlas.r[r];
     sc->cnt.nodes++;
@@ -697,17 +683,15 @@ static void w_scene(const ctx_t* c, int r, ray3* ray, v3 dinv, const int* dsign,
         if (!hit[k]) continue;
         const jt_bvh_node* node = &bvh->nodes[w->child[k]];
         if (node->internal) {
-            w_scene(c, w->rec[k], ray, dinv, dsign, isec, sc);
+            w_scene(c, w->rec[k], ray, dinv, dsign, isec, sc, flip);
             continue;
         }
-        int in_tleaf = 0;
         for (int i = node->start; i < node->start + node->num; i++) {
             int inst_id = bvh->primitives[i];
             sc->cnt.instances++;
             ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], ray);
-            shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc, in_tleaf);
+            shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc, flip);
             if (!s.hit) continue;
-            in_tleaf = 1;
             isec->instance = inst_id;
             isec->element = s.element;
             isec->uv = s.uv;
@@ -718,22 +702,20 @@ static void w_scene(const ctx_t* c, int r, ray3* ray, v3 dinv, const int* dsign,
     }
 }
 /* intersect_scene_bvh on the wide records */
-static scene_isec intersect_scene_wide(const ctx_t* c, ray3 ray, scratch_t* sc) {
+static scene_isec intersect_scene_wide(const ctx_t* c, ray3 ray, scratch_t* sc, int flip) {
     scene_isec isec = {-1, -1, {0, 0}, 0, 0};
-    sc->cnt.rays++;
     if (c->bvh->tlas.nnodes == 0) return isec;
     v3 dinv = V3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
-    int dsign[3] = {(ray.d.x < 0) ^ 1, (ray.d.y < 0) ^ 1, (ray.d.z < 0) ^ 1};
-    w_scene(c, 0, &ray, dinv, dsign, &isec, sc);
+    int dsign[3] = {(ray.d.x < 0) ^ flip, (ray.d.y < 0) ^ flip, (ray.d.z < 0) ^ flip};
+    w_scene(c, 0, &ray, dinv, dsign, &isec, sc, flip);
     return isec;
 }
 /* intersect_instance_bvh on the wide records */
-static scene_isec intersect_instance_wide(const ctx_t* c, int inst_id, ray3 ray, scratch_t* sc) {
+static scene_isec intersect_instance_wide(const ctx_t* c, int inst_id, ray3 ray, scratch_t* sc, int flip) {
     scene_isec isec = {-1, -1, {0, 0}, 0, 0};
-    sc->cnt.light_queries++;
     sc->cnt.instances++;
     ray3 inv_ray = transform_ray(&c->inst_inverse[inst_id], &ray);
-    shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc, 0);
+    shape_isec s = intersect_shape_wide(c, c->scene->instances[inst_id].shape, inv_ray, sc, flip);
     if (!s.hit) return isec;
     isec.instance = inst_id;
     isec.element = s.element;
@@ -742,9 +724,15 @@ static scene_isec intersect_instance_wide(const ctx_t* c, int inst_id, ray3 ray,
     isec.hit = 1;
     return isec;
 }
-/* the traversal jt_params.traversal selects */
+/* the traversal jt_params.traversal selects; a near-first query that saw an exact-t tie runs again
+ * in the reference's child order (the same records) and reports that hit */
 static scene_isec scene_query1(const ctx_t* c, ray3 ray, scratch_t* sc) {
-    return c->params->traversal == JT_TRAVERSAL_WIDE ? intersect_scene_wide(c, ray, sc) : intersect_scene_bvh(c, ray, sc);
+    const int wide = c->params->traversal == JT_TRAVERSAL_WIDE, near = c->params->traversal != JT_TRAVERSAL_REFERENCE;
+    sc->cnt.rays++;
+    sc->tie = 0;
+    scene_isec r = wide ? intersect_scene_wide(c, ray, sc, near) : intersect_scene_bvh(c, ray, sc, near);
+    if (near && sc->tie) r = wide ? intersect_scene_wide(c, ray, sc, 0) : intersect_scene_bvh(c, ray, sc, 0);
+    return r;
 }
 /* or_order_diff: classify the other order's closest hit against this one's, per query */
 static void order_diff(const ctx_t* alt, ray3 ray, scene_isec r, scratch_t* sc) {
@@ -767,8 +755,13 @@ static scene_isec scene_query(const ctx_t* c, ray3 ray, scratch_t* sc) {
     return r;
 }
 static scene_isec instance_query(const ctx_t* c, int inst_id, ray3 ray, scratch_t* sc) {
-    return c->params->traversal == JT_TRAVERSAL_WIDE ? intersect_instance_wide(c, inst_id, ray, sc)
-                                                     : intersect_instance_bvh(c, inst_id, ray, sc);
+    const int wide = c->params->traversal == JT_TRAVERSAL_WIDE, near = c->params->traversal != JT_TRAVERSAL_REFERENCE;
+    sc->cnt.light_queries++;
+    sc->tie = 0;
+    scene_isec r = wide ? intersect_instance_wide(c, inst_id, ray, sc, near) : intersect_instance_bvh(c, inst_id, ray, sc, near);
+    if (near && sc->tie)
+        r = wide ? intersect_instance_wide(c, inst_id, ray, sc, 0) : intersect_instance_bvh(c, inst_id, ray, sc, 0);
+    return r;
 }
 
 /* --------------------------------------------------------------- scene.jl evaluation */
