@@ -13,6 +13,10 @@
 #                              product build), each twice, interleaved
 #   prof:<w>                   rocprofv3 --kernel-trace --stats of a short bench run of workload <w>
 #   stamps:<w>                 the JT_STAMPS build's per-phase wave clocks (scripts/stamps.py)
+#   tdmix[:<args>]             the vector-memory gather ceilings (scripts/td_mix_bench.hip, built
+#                              by `make -C julia-raytracer_amd td-mix`): rates, then TD busy / L2 hits
+#   rehearse:<N>               N ranks of bench.py under torch.distributed.run on this one GPU,
+#                              reducing through gloo (RCCL cannot put two ranks on one GPU)
 #   host                       the box's CPU description
 # workloads: cb (the headline, cornellbox path 1280x720x256), cb1 (config 1: naive 256x256x16),
 #   f2 (features2 1920x1080x512), b1 (bathroom1 1920x1080x1024), ec (ecosys 3840x2160 at 64 spp),
@@ -68,9 +72,9 @@ for task in "$@"; do
     case $kind in
         tests)
             if [ -n "$rest" ]; then
-                $S 1100 "$O/pytest.log" python -u -m pytest tests -x -v -m gpu -rf --timeout 240 --timeout-method thread -k "$rest" || exit 1
+                $S 1100 "$O/pytest.log" python -u -m pytest tests -x -v -m gpu -rf -rP --timeout 240 --timeout-method thread -k "$rest" || exit 1
             else
-                $S 1100 "$O/pytest.log" python -u -m pytest tests -x -v -m gpu -rf --timeout 240 --timeout-method thread || exit 1
+                $S 1100 "$O/pytest.log" python -u -m pytest tests -x -v -m gpu -rf -rP --timeout 240 --timeout-method thread || exit 1
             fi ;;
         smoke)
             $S 300 "$O/smoke.log" python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
@@ -96,6 +100,12 @@ for task in "$@"; do
             $S 300 "$O/prof_$name.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$name" -o kt -- python3 bench.py --no-cpu-baseline --no-reference-order $(wargs "$w") --steps 2 --warmup 1 || exit 1 ;;
         stamps)
             $S 400 "$O/stamps_$name.log" python scripts/stamps.py $(wargs "$w") || exit 1 ;;
+        tdmix)
+            TD=julia-raytracer_amd/build/td_mix_bench
+            $S 200 "$O/tdmix_rates$name.log" timeout -k 10 180 $TD $w $extra || exit 1
+            $S 200 "$O/tdmix_pmc$name.log" timeout -s KILL 180 rocprofv3 --pmc TD_TD_BUSY_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d "$O/tdmix_pmc$name" -o pmc -- $TD $w $extra || exit 1 ;;
+        rehearse)
+            JT_BENCH_BACKEND=gloo JT_BENCH_DEVICE=0 $S 300 "$O/rehearsal_n${w}_gloo_one_gpu.log" python -m torch.distributed.run --nnodes=1 --nproc-per-node "$w" --master-addr 127.0.0.1 --master-port $((29500 + w)) bench.py --gpus "$w" --steps 3 --warmup 1 --no-cpu-baseline || exit 1 ;;
         host)
             { nproc; lscpu | grep -E "Model name|Socket|Core|Thread"; rocm-smi --showproductname 2>/dev/null | head -20; } > "$O/host.txt" 2>&1 ;;
         *) echo "unknown task $task" >&2; exit 2 ;;
