@@ -75,15 +75,19 @@ typedef enum jt_sampler { JT_SAMPLER_PATH = 1, JT_SAMPLER_NAIVE = 2 } jt_sampler
  *   start then start+1, so the upper child (start+1, higher split-axis coordinates: split_middle /
  *   split_sah partition lower centers to `start`, src/bvh.jl:171-176, 281-304) is visited first —
  *   the far child for a closest-hit query.
- * JT_TRAVERSAL_NEAR: the opposite push order, the near child by the split axis first. The closest
- *   hit is the same up to ties: among hits at exactly equal t the later-tested wins
- *   (src/geometry.jl:226, t > tmax rejects), so only exact-t ties (and a box culled by the slab
- *   test's rounding) can resolve differently. Fewer nodes are visited (tmax shrinks sooner).
+ * JT_TRAVERSAL_NEAR: the opposite push order, the near child by the split axis first. Fewer nodes
+ *   are visited (tmax shrinks sooner). Among hits at exactly equal t the reference's later-tested
+ *   one wins (src/geometry.jl:226, t > tmax rejects), which depends on the order: a near-first
+ *   query that accepts a hit at exactly its current tmax is run again in the reference's child
+ *   order and reports that hit. The closest hit then differs from the reference's only where the
+ *   slab test's rounding lets one order find a hit the other culls (measured: 2e-6 of bathroom1's
+ *   paths, none on cornellbox, features2, ecosys).
  * JT_TRAVERSAL_WIDE: the reference's binary tree collapsed to 4-wide records (each internal node
  *   holds its grandchildren: same leaves, same primitive order) with conservative 8-bit quantised
- *   child boxes, visited near child first in the binary DFS order. A box can only pass where the
- *   exact one would, or more often, so again only exact-t ties and boxes the exact slab test culls
- *   by rounding can resolve differently; one 64-B record replaces about three 32-B node visits. */
+ *   child boxes, visited near child first in the binary DFS order (a tie's re-run: far child
+ *   first, the reference's leaf sequence). A box can only pass where the exact one would, or more
+ *   often, so again only boxes the exact slab test culls by rounding can resolve differently; one
+ *   64-B record replaces about three 32-B node visits. */
 typedef enum jt_traversal {
     JT_TRAVERSAL_REFERENCE = 0,
     JT_TRAVERSAL_NEAR = 1,
