@@ -4,6 +4,7 @@
 //   mode 1: a 64-B wide node record (4 x dwordx4)     node_step_wide
 //   mode 2: an 80-B triangle pair (5 x dwordx4)       prim_step
 //   mode 3: an 8-B texel pair (dwordx2)               eval_texture
+//   mode 4: a 48-B compact wide record (3 x dwordx4)  (candidate: child words packed into row 2)
 // over working sets from L2-resident (4 MiB per XCD) through MALL (64-256 MiB) to HBM (2 GiB).
 // Every lane walks its own chain (the next record index from the loaded words); all 64 lanes are
 // active (td_lanes_bench: the TD charges per wave-instruction, not per active lane). Prints the
@@ -38,6 +39,10 @@ __global__ __launch_bounds__(256) void chase(const uint4* rec, unsigned n, int s
             const uint4* r = rec + 5 * (size_t)i;
             const uint4 a = r[0], b = r[1], c = r[2], d = r[3], e = r[4];
             v = a.x ^ b.y ^ c.z ^ d.w ^ e.x ^ a.w ^ b.x ^ c.y ^ d.z ^ e.w;
+        } else if (MODE == 4) {
+            const uint4* r = rec + 3 * (size_t)i;
+            const uint4 a = r[0], b = r[1], c = r[2];
+            v = a.x ^ b.y ^ c.z ^ a.w ^ b.x ^ c.y;
         } else {
             const uint2 a = reinterpret_cast<const uint2*>(rec)[(size_t)i];
             v = a.x ^ a.y;
@@ -83,18 +88,19 @@ int main(int argc, char** argv) {
     if (lds > 0) (void)hipFuncSetAttribute((const void*)chase<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                  (void)hipFuncSetAttribute((const void*)chase<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                  (void)hipFuncSetAttribute((const void*)chase<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                 (void)hipFuncSetAttribute((const void*)chase<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                 (void)hipFuncSetAttribute((const void*)chase<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                 (void)hipFuncSetAttribute((const void*)chase<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     printf("workgroups per CU %d (LDS %zu B each), active lanes per wave %d\n", per_cu, lds, active);
     if (hipMalloc(&rec, max_bytes) != hipSuccess || hipMalloc(&out, (size_t)blocks * 256 * 4) != hipSuccess) return 1;
     fill<<<4096, 256>>>(rec, max_bytes / 16);
     if (hipDeviceSynchronize() != hipSuccess) return 1;
     const size_t sets[4] = {4ull << 20, 64ull << 20, 256ull << 20, 2ull << 30};
-    const char* name[4] = {"16 B row (dwordx4)", "64 B wide node (4 x dwordx4)", "80 B tri pair (5 x dwordx4)",
-                           "8 B texel pair (dwordx2)"};
-    const int insts[4] = {1, 4, 5, 1};
-    const int rec_bytes[4] = {16, 64, 80, 8};
+    const char* name[5] = {"16 B row (dwordx4)", "64 B wide node (4 x dwordx4)", "80 B tri pair (5 x dwordx4)",
+                           "8 B texel pair (dwordx2)", "48 B compact wide (3 x dwordx4)"};
+    const int insts[5] = {1, 4, 5, 1, 3};
+    const int rec_bytes[5] = {16, 64, 80, 8, 48};
     run<0>(rec, 1u << 16, out, blocks, 200, active, lds);  // warm-up dispatch
-    for (int m = 0; m < 4; m++) {
+    for (int m = 0; m < 5; m++) {
         for (int w = 0; w < 4; w++) {
             unsigned n = 1;
             while ((size_t)(n * 2ull) * rec_bytes[m] <= sets[w]) n *= 2;
@@ -102,7 +108,8 @@ int main(int argc, char** argv) {
             float ms = m == 0 ? run<0>(rec, n, out, blocks, steps, active, lds)
                      : m == 1 ? run<1>(rec, n, out, blocks, steps, active, lds)
                      : m == 2 ? run<2>(rec, n, out, blocks, steps, active, lds)
-                              : run<3>(rec, n, out, blocks, steps, active, lds);
+                     : m == 3 ? run<3>(rec, n, out, blocks, steps, active, lds)
+                              : run<4>(rec, n, out, blocks, steps, active, lds);
             const double waves = (double)blocks * 4 * steps;  // 4 waves per workgroup
             printf("mode %d %-30s set %5zu MiB  %8.2f ms  %8.2f G wave-instr/s  %8.1f G records/s\n", m, name[m],
                    ((size_t)n * rec_bytes[m]) >> 20, ms, waves * insts[m] / ms * 1e-6,
