@@ -302,18 +302,53 @@ float exp_scale(int e) {  // 2^(e - 127), e = a normal float's biased exponent
     std::memcpy(&f, &b, 4);
     return f;
 }
+// The binary leaves of a tree in the order the wide records list them: records breadth-first (as
+// build_wide appends them), within a record its leaf children in slot order. The device lays out
+// primitive records and numbers instances in this order, so a record's leaf children are
+// consecutive runs (JT_WIDE48 records address them from one start) and every binary leaf is
+// still one run (the binary traversal addresses a leaf by its start).
+std::vector<int> wide_leaf_order(const jt_bvh_tree& t) {
+    std::vector<int> order;
+    if (t.nnodes <= 0) return order;
+    if (!t.nodes[0].internal) {
+        order.push_back(0);
+        return order;
+    }
+    std::vector<int> q{0};
+    for (size_t h = 0; h < q.size(); h++) {
+        const jt_bvh_node& N = t.nodes[q[h]];
+        int slot[4] = {-1, -1, -1, -1};
+        const int L = N.start, R = N.start + 1;
+        if (t.nodes[L].internal) slot[0] = t.nodes[L].start, slot[1] = t.nodes[L].start + 1;
+        else slot[0] = L;
+        if (t.nodes[R].internal) slot[2] = t.nodes[R].start, slot[3] = t.nodes[R].start + 1;
+        else slot[2] = R;
+        for (int c = 0; c < 4; c++) {
+            if (slot[c] < 0) continue;
+            if (t.nodes[slot[c]].internal) q.push_back(slot[c]);
+            else order.push_back(slot[c]);
+        }
+    }
+    return order;
+}
+
 // The wide records of one binary tree, appended to `out` breadth-first (global indices =
 // positions in `out`). A record stands for an internal node N (or the root leaf) and holds N's
 // grandchildren in slots [LL, LR, RL, RR] (a leaf child takes the pair's first slot alone), their
 // boxes quantised relative to N's box per axis at the smallest scale 2^(e-127) >= extent / 255
 // (and the next larger ones until every child fits). leaf_word(k): the child word of binary leaf
 // k. Returns the root record's index, or -1 with the error set.
-int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_word, std::vector<DWide>& out) {
+int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_word, const std::function<int(int)>& leaf_units,
+               std::vector<DWide>& out) {
     if (t.nnodes <= 0 || (!t.nodes[0].internal && t.nodes[0].num <= 0)) {
         // an empty tree (make_bvh of no boxes is one leaf without primitives, src/bvh.jl:138-183):
         // one record without children, so a query visits it and finds nothing
         DWide w{};
+#if JT_WIDE48
+        w.r2 = make_uint4(0u, 0u, 0u, 0u);  // every slot empty
+#else
         w.r3 = make_uint4(W_EMPTY, W_EMPTY, W_EMPTY, W_EMPTY);
+#endif
         out.push_back(w);
         return (int)out.size() - 1;
     }
@@ -386,8 +421,36 @@ int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_wo
                               ((unsigned)(N.internal ? N.axis : 0) | (unsigned)a1 << 2 | (unsigned)a2 << 4) << 24;
         W.r0 = make_float4(N.bmin[0], N.bmin[1], N.bmin[2], as_f(meta));
         W.r1 = make_uint4(bytes(lo[0]), bytes(hi[0]), bytes(lo[1]), bytes(hi[1]));
+#if JT_WIDE48
+        // children from two words: the first internal child's record (internal children's records
+        // are consecutive) and the first leaf child's start (leaf children's runs are consecutive,
+        // wide_leaf_order), with a kind nibble per slot (0 empty, 1 internal, 8 | n-1 a leaf of n)
+        unsigned first_rec = 0, first_leaf = 0, kinds = 0, next = 0;
+        bool have_leaf = false;
+        for (int c = 0; c < 4; c++) {
+            if (slot[c] < 0) continue;
+            if (t.nodes[slot[c]].internal) {
+                kinds |= 1u << (4 * c);
+                continue;
+            }
+            const unsigned start = word[c] & (W_START & IDX_MASK);
+            if (!have_leaf) first_leaf = next = start, have_leaf = true;
+            if (start != next) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: leaf runs not consecutive"), -1;
+            next += (unsigned)leaf_units(slot[c]);
+            kinds |= (8u | (unsigned)(t.nodes[slot[c]].num - 1)) << (4 * c);
+        }
+        for (int c = 0; c < 4; c++)
+            if (slot[c] >= 0 && t.nodes[slot[c]].internal) {
+                first_rec = word[c];  // the first internal slot's record; the others follow it
+                break;
+            }
+        if (first_rec > IDX_MASK || first_leaf > IDX_MASK)
+            return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: record or leaf start above 2^24"), -1;
+        W.r2 = make_uint4(bytes(lo[2]), bytes(hi[2]), first_rec | (kinds & 0xffu) << 24, first_leaf | (kinds >> 8) << 24);
+#else
         W.r2 = make_uint4(bytes(lo[2]), bytes(hi[2]), 0u, 0u);
         W.r3 = make_uint4(word[0], word[1], word[2], word[3]);
+#endif
     }
     return rec[0];
 }
@@ -536,13 +599,25 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     }
     int st = check_tree(bvh->tlas, scene->ninstances, "tlas");
     if (st != JT_OK) return st;
-    // the device numbers instances in TLAS leaf order (a leaf's instances are then the id range
-    // start .. start+num-1, no per-instance index load): the TLAS must list each instance once
+    // the device numbers instances by TLAS leaf, leaves in wide-record order (wide_leaf_order), a
+    // leaf's instances in its own order: a leaf's instances are then the id range start ..
+    // start+num-1 (no per-instance index load) and a wide record's leaf children one range. The
+    // TLAS must list each instance once.
     std::vector<int> inst_new(scene->ninstances, -1);  // reference instance id -> device id
-    for (int k = 0; k < bvh->tlas.nprimitives; k++) {
-        int& slot = inst_new[bvh->tlas.primitives[k]];
-        if (slot >= 0) return jt::fail(JT_ERR_INVALID, "tlas: an instance is listed twice");
-        slot = k;
+    std::vector<int> tleaf_start(std::max(0, bvh->tlas.nnodes), 0);  // binary TLAS leaf -> first device id
+    {
+        int next = 0;
+        for (int k : wide_leaf_order(bvh->tlas)) {
+            const jt_bvh_node& n = bvh->tlas.nodes[k];
+            tleaf_start[k] = next;
+            for (int q = 0; q < n.num; q++) {
+                int& slot = inst_new[bvh->tlas.primitives[n.start + q]];
+                if (slot >= 0) return jt::fail(JT_ERR_INVALID, "tlas: an instance is listed twice");
+                slot = next++;
+            }
+        }
+        for (int& v : inst_new)  // instances no TLAS leaf lists are never visited
+            if (v < 0) v = next++;
     }
     if (st != JT_OK) return st;
     int max_blas_depth = 0;
@@ -629,7 +704,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         tlas.resize(order.size());
         for (size_t q = 0; q < order.size(); q++) {
             const jt_bvh_node& n = bvh->tlas.nodes[order[q]];
-            tlas[q] = pack_node(n, n.internal ? newidx[n.start] : n.start);
+            tlas[q] = pack_node(n, n.internal ? newidx[n.start] : tleaf_start[order[q]]);
         }
     }
     std::vector<DNode> blas;
@@ -700,22 +775,29 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                                           d.pos_base + sh.quads[4 * k + 2], d.pos_base + sh.quads[4 * k + 3]));
         }
         auto P3 = [&](int vi) { return f4(sh.positions[3 * vi], sh.positions[3 * vi + 1], sh.positions[3 * vi + 2], 0); };
-        if (d.kind == KIND_TRI) {
-            // Triangle-pair records, leaf by leaf (a leaf starts a record; an odd leaf's last
-            // record has a zero second triangle, never accepted: the leaf count masks it). The
-            // two triangles' components are interleaved so the pair test runs on packed FP32:
-            //   (p1x p1x' p1y p1y') (p1z p1z' e1x e1x') (e1y e1y' e1z e1z') (e2x e2x' e2y e2y')
-            //   (e2z e2z' el el'), edge1 = p2 - p1, edge2 = p3 - p1 (src/geometry.jl:208-209).
-            // The records hold the reference's floats for bvh.primitives[i], pre-gathered.
-            int pairs = 0;
-            for (int k = 0; k < t.nnodes; k++) {
-                const jt_bvh_node& n = t.nodes[k];
-                if (n.internal) {
-                    blas.push_back(pack_node(n, d.blas_root + n.start));
-                    continue;
-                }
-                blas.push_back(pack_node(n, d.prim_base + pairs));
-                leaf_rec[s][k] = d.prim_base + pairs;
+        // records leaf by leaf, the leaves in wide-record order (wide_leaf_order: a wide record's
+        // leaf children are consecutive runs); a leaf's records are its primitives in the
+        // reference's order (bvh.primitives[start .. start+num-1]), pre-gathered
+        const std::vector<int> lorder = wide_leaf_order(t);
+        {
+            int at = 0;
+            for (int k : lorder) {
+                leaf_rec[s][k] = d.prim_base + at;
+                at += d.kind == KIND_TRI ? (t.nodes[k].num + 1) / 2 : t.nodes[k].num;
+            }
+        }
+        for (int k = 0; k < t.nnodes; k++) {
+            const jt_bvh_node& n = t.nodes[k];
+            blas.push_back(pack_node(n, n.internal ? d.blas_root + n.start : std::max(0, leaf_rec[s][k])));
+        }
+        for (int k : lorder) {
+            const jt_bvh_node& n = t.nodes[k];
+            if (d.kind == KIND_TRI) {
+                // Triangle-pair records (a leaf starts a record; an odd leaf's last record has a
+                // zero second triangle, never accepted: the leaf count masks it). The two
+                // triangles' components are interleaved so the pair test runs on packed FP32:
+                //   (p1x p1x' p1y p1y') (p1z p1z' e1x e1x') (e1y e1y' e1z e1z') (e2x e2x' e2y e2y')
+                //   (e2z e2z' el el'), edge1 = p2 - p1, edge2 = p3 - p1 (src/geometry.jl:208-209).
                 for (int q = 0; q < n.num; q += 2) {
                     float4 p[2], e1[2], e2[2];
                     int el[2] = {-1, -1};
@@ -734,29 +816,22 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                     prims.push_back(f4(e1[0].y, e1[1].y, e1[0].z, e1[1].z));
                     prims.push_back(f4(e2[0].x, e2[1].x, e2[0].y, e2[1].y));
                     prims.push_back(f4(e2[0].z, e2[1].z, as_f(el[0]), as_f(el[1])));
-                    pairs++;
+                }
+            } else {
+                // quad records (the reference reads positions through bvh.primitives[i])
+                for (int q = 0; q < n.num; q++) {
+                    const int el = t.primitives[n.start + q];
+                    const int* v = &sh.quads[4 * el];
+                    float4 a = P3(v[0]), b = P3(v[1]), cc = P3(v[2]), dd = P3(v[3]);
+                    a.w = as_f(el);
+                    const bool degenerate = cc.x == dd.x && cc.y == dd.y && cc.z == dd.z;  // p3 == p4
+                    dd.w = degenerate ? 1.0f : 0.0f;
+                    prims.push_back(a);
+                    prims.push_back(b);
+                    prims.push_back(cc);
+                    prims.push_back(dd);
                 }
             }
-            continue;
-        }
-        for (int k = 0; k < t.nnodes; k++) {
-            const jt_bvh_node& n = t.nodes[k];
-            blas.push_back(pack_node(n, n.internal ? d.blas_root + n.start : d.prim_base + n.start));
-            if (!n.internal) leaf_rec[s][k] = d.prim_base + n.start;
-        }
-        // quad records in BVH leaf order (the reference reads positions through
-        // bvh.primitives[i]; the records hold the same floats, pre-gathered)
-        for (int k = 0; k < t.nprimitives; k++) {
-            const int el = t.primitives[k];
-            const int* v = &sh.quads[4 * el];
-            float4 a = P3(v[0]), b = P3(v[1]), cc = P3(v[2]), dd = P3(v[3]);
-            a.w = as_f(el);
-            const bool degenerate = cc.x == dd.x && cc.y == dd.y && cc.z == dd.z;  // p3 == p4
-            dd.w = degenerate ? 1.0f : 0.0f;
-            prims.push_back(a);
-            prims.push_back(b);
-            prims.push_back(cc);
-            prims.push_back(dd);
         }
     }
     // wide records (JT_TRAVERSAL_WIDE): the TLAS's, then every BLAS's; the binary node array is
@@ -772,18 +847,17 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     auto build_all_wide = [&]() -> int {
         const int r = build_wide(bvh->tlas, [&](int k) -> unsigned {
             const jt_bvh_node& n = bvh->tlas.nodes[k];
-            if (n.start < 0 || n.start > (int)W_START - 1) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: instance id too large"), (unsigned)W_EMPTY;
-            return W_LEAF | W_INST | (unsigned)(n.num - 1) << 28 | (unsigned)n.start;
-        }, wnodes);
+            return W_LEAF | W_INST | (unsigned)(n.num - 1) << 28 | (unsigned)tleaf_start[k];
+        }, [&](int k) { return (int)bvh->tlas.nodes[k].num; }, wnodes);
         if (r < 0) return JT_ERR_UNSUPPORTED;
         tlas_wnodes = (int)wnodes.size();
         for (int s = 0; s < scene->nshapes; s++) {
             const jt_bvh_tree& t = bvh->blas[s];
             wroot[s] = build_wide(t, [&](int k) -> unsigned {
                 const int st0 = leaf_rec[s][k];
-                if (st0 < 0 || st0 > (int)W_START - 1) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: too many primitive records"), (unsigned)W_EMPTY;
+                if (st0 < 0 || st0 > (int)IDX_MASK) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: too many primitive records"), (unsigned)W_EMPTY;
                 return W_LEAF | (unsigned)(t.nodes[k].num - 1) << 28 | (unsigned)st0;
-            }, wnodes);
+            }, [&](int k) { return shapes[s].kind == KIND_TRI ? (t.nodes[k].num + 1) / 2 : (int)t.nodes[k].num; }, wnodes);
             if (wroot[s] < 0) return JT_ERR_UNSUPPORTED;
         }
         return JT_OK;
