@@ -51,21 +51,10 @@ struct alignas(16) DNode {
 // child word: W_EMPTY; bit 31 clear: a record index; bit 31 set: a leaf, bit 30 set for a TLAS
 // leaf (instances start .. start + num - 1), bits 28-29 num - 1, bits 0-27 start (first instance,
 // triangle-pair record or quad record)
-// JT_WIDE48: 48-B records, three 16-B loads per visit instead of four. Row 3's four child words
-// are replaced by two words in row 2's free half: z = the first internal child's record (internal
-// children's records are consecutive) | kind nibbles of slots 0, 1 << 24; w = the first leaf
-// child's start (leaf children's runs are consecutive: the host lays out primitive records and
-// numbers instances in wide_leaf_order) | kind nibbles of slots 2, 3 << 24. Kind: 0 empty, 1
-// internal, 8 | (n - 1) a leaf of n primitives / instances.
-#ifndef JT_WIDE48
-#define JT_WIDE48 0
-#endif
 struct alignas(16) DWide {
     float4 r0;
     uint4 r1, r2;
-#if !JT_WIDE48
     uint4 r3;
-#endif
 };
 enum : unsigned { W_EMPTY = 0xffffffffu, W_LEAF = 0x80000000u, W_INST = 0x40000000u, W_START = 0x0fffffffu };
 // Traversal record of an instance, 64 B: inverse(frame, true) as 12 floats + ids.

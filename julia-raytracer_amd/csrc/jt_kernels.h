@@ -700,25 +700,6 @@ __device__ __forceinline__ int wide_slot(unsigned flips, int k) {
 __device__ __forceinline__ unsigned wide_word(const uint4& r3, int slot) {
     return slot == 0 ? r3.x : slot == 1 ? r3.y : slot == 2 ? r3.z : r3.w;
 }
-// JT_WIDE48: the child word of `slot` from row 2's z / w words (DWide, jt_device.h). A leaf's
-// run is one record per instance (TLAS records) or quad, or one per triangle pair
-__device__ __forceinline__ unsigned w48_word(unsigned z, unsigned w, int slot, bool tlas, bool quad) {
-    const bool unit1 = tlas || quad;
-    const unsigned kinds = (z >> 24) | ((w >> 24) << 8);
-    const unsigned ks = (kinds >> (4 * slot)) & 15u;
-    unsigned nint = 0, off = 0;
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        if (j >= slot) break;
-        const unsigned kj = (kinds >> (4 * j)) & 15u;
-        nint += kj == 1u ? 1u : 0u;
-        const unsigned n = (kj & 7u) + 1u;
-        off += kj >= 8u ? (unit1 ? n : (n + 1u) >> 1) : 0u;
-    }
-    if (ks == 0u) return W_EMPTY;
-    if (ks == 1u) return (z & IDX_MASK) + nint;
-    return W_LEAF | (tlas ? W_INST : 0u) | (ks & 7u) << 28 | ((w & IDX_MASK) + off);
-}
 // dequantised box of slot c (the record's origin + byte * scale, in float) as intersect_bbox's
 // (bmin.x, bmax.x, bmin.y, bmax.y), (bmin.z, bmax.z). byte * scale is exact (a byte times a
 // normal power of two), so the fused multiply-add rounds once exactly as origin + byte * scale
@@ -763,13 +744,7 @@ __device__ __forceinline__ void wide_visit(const DScene& S, Trav& T, int* stack,
     if (COUNT) cnt.nodes++;
     const DWide& rec = S.wnodes[idx];
     const float4 r0 = rec.r0;
-#if JT_WIDE48
-    const uint4 r1 = rec.r1, r2 = rec.r2;
-    const bool tlas = idx < (unsigned)S.tlas_wnodes;
-    const unsigned kinds = (r2.z >> 24) | ((r2.w >> 24) << 8);
-#else
     const uint4 r1 = rec.r1, r2 = rec.r2, r3 = rec.r3;
-#endif
     const unsigned meta = __float_as_uint(r0.w);
     const float sx = __uint_as_float((meta & 255u) << 23), sy = __uint_as_float(((meta >> 8) & 255u) << 23),
                 sz = __uint_as_float(((meta >> 16) & 255u) << 23);
@@ -779,11 +754,7 @@ __device__ __forceinline__ void wide_visit(const DScene& S, Trav& T, int* stack,
         float4 a, b;
         wide_box(r0, r1, r2, sx, sy, sz, c, a, b);
         const bool pass = intersect_bbox(T.lo, T.ldinv, ray_eps, T.tmax, a, b);
-#if JT_WIDE48
-        if (((kinds >> (4 * c)) & 15u) != 0u && pass) hits |= 1u << c;
-#else
         if (wide_word(r3, c) != W_EMPTY && pass) hits |= 1u << c;
-#endif
     }
     if (!hits) return;
     const unsigned ax = meta >> 24;
@@ -795,11 +766,7 @@ __device__ __forceinline__ void wide_visit(const DScene& S, Trav& T, int* stack,
     const int k0 = __builtin_ctz(vm);
     const unsigned rest = vm & (vm - 1u);
     if (rest) st_push<RING, OVF>(S, T, stack, pixel, flips << 28 | rest << 24 | idx);
-#if JT_WIDE48
-    wide_take<F>(T, w48_word(r2.z, r2.w, wide_slot(flips, k0), tlas, (F & FT_QUAD) && T.cur_kind == KIND_QUAD));
-#else
     wide_take<F>(T, wide_word(r3, wide_slot(flips, k0)));
-#endif
 }
 // One node step of the wide traversal: the pending child word, or the next child of the group on
 // top of the stack (its word: one 4-B load), or the next instance of a range. An instance visit
@@ -817,13 +784,7 @@ __device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* st
             const unsigned rest = m & (m - 1u);
             if (rest) st_push<RING, OVF>(S, T, stack, pixel, (e & ~(15u << 24)) | rest << 24);
             if (XF && T.inst_space && idx < (unsigned)S.tlas_wnodes) world_ray(S, T);  // back in the TLAS
-#if JT_WIDE48
-            const uint2 zw = reinterpret_cast<const uint2*>(S.wnodes + idx)[5];
-            w = w48_word(zw.x, zw.y, wide_slot((e >> 28) & 7u, __builtin_ctz(m)), idx < (unsigned)S.tlas_wnodes,
-                         (F & FT_QUAD) && T.cur_kind == KIND_QUAD);
-#else
             w = reinterpret_cast<const unsigned*>(S.wnodes + idx)[12 + wide_slot((e >> 28) & 7u, __builtin_ctz(m))];
-#endif
             if ((w & (W_LEAF | W_INST)) == W_LEAF) {
                 wide_take<F>(T, w);
                 return;

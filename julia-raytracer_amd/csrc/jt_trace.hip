@@ -305,8 +305,11 @@ float exp_scale(int e) {  // 2^(e - 127), e = a normal float's biased exponent
 // The binary leaves of a tree in the order the wide records list them: records breadth-first (as
 // build_wide appends them), within a record its leaf children in slot order. The device lays out
 // primitive records and numbers instances in this order, so a record's leaf children are
-// consecutive runs (JT_WIDE48 records address them from one start) and every binary leaf is
-// still one run (the binary traversal addresses a leaf by its start).
+// consecutive runs (a record could address them from one start) and every binary leaf is
+// still one run (the binary traversal addresses a leaf by its start). Measured against node-index
+// order: bathroom1 even, ecosys even (profiles/r05_ab/wide48_vs_wide64_r05f.txt "base"); it is
+// what a record addressing its leaf children from one start needs (the 48-B record experiment,
+// DESIGN.md §2).
 std::vector<int> wide_leaf_order(const jt_bvh_tree& t) {
     std::vector<int> order;
     if (t.nnodes <= 0) return order;
@@ -338,17 +341,12 @@ std::vector<int> wide_leaf_order(const jt_bvh_tree& t) {
 // boxes quantised relative to N's box per axis at the smallest scale 2^(e-127) >= extent / 255
 // (and the next larger ones until every child fits). leaf_word(k): the child word of binary leaf
 // k. Returns the root record's index, or -1 with the error set.
-int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_word, const std::function<int(int)>& leaf_units,
-               std::vector<DWide>& out) {
+int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_word, std::vector<DWide>& out) {
     if (t.nnodes <= 0 || (!t.nodes[0].internal && t.nodes[0].num <= 0)) {
         // an empty tree (make_bvh of no boxes is one leaf without primitives, src/bvh.jl:138-183):
         // one record without children, so a query visits it and finds nothing
         DWide w{};
-#if JT_WIDE48
-        w.r2 = make_uint4(0u, 0u, 0u, 0u);  // every slot empty
-#else
         w.r3 = make_uint4(W_EMPTY, W_EMPTY, W_EMPTY, W_EMPTY);
-#endif
         out.push_back(w);
         return (int)out.size() - 1;
     }
@@ -421,36 +419,8 @@ int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_wo
                               ((unsigned)(N.internal ? N.axis : 0) | (unsigned)a1 << 2 | (unsigned)a2 << 4) << 24;
         W.r0 = make_float4(N.bmin[0], N.bmin[1], N.bmin[2], as_f(meta));
         W.r1 = make_uint4(bytes(lo[0]), bytes(hi[0]), bytes(lo[1]), bytes(hi[1]));
-#if JT_WIDE48
-        // children from two words: the first internal child's record (internal children's records
-        // are consecutive) and the first leaf child's start (leaf children's runs are consecutive,
-        // wide_leaf_order), with a kind nibble per slot (0 empty, 1 internal, 8 | n-1 a leaf of n)
-        unsigned first_rec = 0, first_leaf = 0, kinds = 0, next = 0;
-        bool have_leaf = false;
-        for (int c = 0; c < 4; c++) {
-            if (slot[c] < 0) continue;
-            if (t.nodes[slot[c]].internal) {
-                kinds |= 1u << (4 * c);
-                continue;
-            }
-            const unsigned start = word[c] & (W_START & IDX_MASK);
-            if (!have_leaf) first_leaf = next = start, have_leaf = true;
-            if (start != next) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: leaf runs not consecutive"), -1;
-            next += (unsigned)leaf_units(slot[c]);
-            kinds |= (8u | (unsigned)(t.nodes[slot[c]].num - 1)) << (4 * c);
-        }
-        for (int c = 0; c < 4; c++)
-            if (slot[c] >= 0 && t.nodes[slot[c]].internal) {
-                first_rec = word[c];  // the first internal slot's record; the others follow it
-                break;
-            }
-        if (first_rec > IDX_MASK || first_leaf > IDX_MASK)
-            return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: record or leaf start above 2^24"), -1;
-        W.r2 = make_uint4(bytes(lo[2]), bytes(hi[2]), first_rec | (kinds & 0xffu) << 24, first_leaf | (kinds >> 8) << 24);
-#else
         W.r2 = make_uint4(bytes(lo[2]), bytes(hi[2]), 0u, 0u);
         W.r3 = make_uint4(word[0], word[1], word[2], word[3]);
-#endif
     }
     return rec[0];
 }
@@ -848,7 +818,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         const int r = build_wide(bvh->tlas, [&](int k) -> unsigned {
             const jt_bvh_node& n = bvh->tlas.nodes[k];
             return W_LEAF | W_INST | (unsigned)(n.num - 1) << 28 | (unsigned)tleaf_start[k];
-        }, [&](int k) { return (int)bvh->tlas.nodes[k].num; }, wnodes);
+        }, wnodes);
         if (r < 0) return JT_ERR_UNSUPPORTED;
         tlas_wnodes = (int)wnodes.size();
         for (int s = 0; s < scene->nshapes; s++) {
@@ -857,7 +827,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
                 const int st0 = leaf_rec[s][k];
                 if (st0 < 0 || st0 > (int)IDX_MASK) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: too many primitive records"), (unsigned)W_EMPTY;
                 return W_LEAF | (unsigned)(t.nodes[k].num - 1) << 28 | (unsigned)st0;
-            }, [&](int k) { return shapes[s].kind == KIND_TRI ? (t.nodes[k].num + 1) / 2 : (int)t.nodes[k].num; }, wnodes);
+            }, wnodes);
             if (wroot[s] < 0) return JT_ERR_UNSUPPORTED;
         }
         return JT_OK;

@@ -68,7 +68,7 @@ for task in "$@"; do
     w=${rest%%:*}
     extra=${rest#*:}
     [ "$extra" = "$rest" ] && extra=""
-    name=$(echo "$w" | tr '/' '_')
+    name=$(echo "$w${extra:+_$extra}" | tr '/ ' '__')
     case $kind in
         tests)
             if [ -n "$rest" ]; then
