@@ -391,14 +391,6 @@ struct Trav {
 #define JT_TIE_RERUN 1  // 0: ties resolve in the near-first order's own sequence (A/B runs only)
 #endif
 constexpr int TIE_SEEN = 1 << 8, REF_RERUN = 1 << 9, NH_COUNT = 63;
-// JT_MAT_DEFER (experiment, SURVEY §8(f) rank 3 "material sorting"): in a shading phase of a scene
-// with several material types, surface hits whose type is not the phase's most common one wait
-// for a later phase (once; MAT_DEFERRED) and do not count toward the shading gate meanwhile, so a
-// phase runs fewer BSDF branches. Scheduling only: results are bit-identical.
-#ifndef JT_MAT_DEFER
-#define JT_MAT_DEFER 0
-#endif
-constexpr int MAT_DEFERRED = 1 << 10;
 // the child-order flip of the lane's current query: near-first, unless it is a tie's re-run
 __device__ __forceinline__ int query_flip(const DScene& S, const Trav& T) { return (T.nh & REF_RERUN) ? 0 : S.order_flip; }
 // a hit accepted at t (t <= tmax): count it (child pre-test snapshots) and note an exact-t tie
@@ -1614,7 +1606,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
         for (;;) {
             const bool wantp = T.nprim > 0;
             const bool wantn = wants_node<WIDE>(T);
-            const bool waiting = query_done<WIDE>(T) && !(JT_MAT_DEFER && (F & FT_MAT) && (T.nh & MAT_DEFERRED));
+            const bool waiting = query_done<WIDE>(T);
             const int np = lane_count(__builtin_amdgcn_ballot_w64(wantp));
             const int nn = lane_count(__builtin_amdgcn_ballot_w64(wantn));
             int nw = lane_count(__builtin_amdgcn_ballot_w64(waiting));
@@ -1710,21 +1702,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
         }
         bool c_path = false, c_lq = false, c_ray = false;
         unsigned n_inl = 0;
-        bool defer = false;
-        if constexpr (JT_MAT_DEFER && (F & FT_MAT) != 0) {
-            // the phase's most common material type among fresh surface hits; the others wait once
-            const bool cand = query_done<WIDE>(T) && st.phase == PH_SCENE && T.h_inst >= 0 && !(T.nh & MAT_DEFERRED);
-            const int mt = cand ? row16<F>(&S.inst_shade[T.h_inst].material).z : -1;
-            int best = -1, bestn = 0;
-#pragma unroll
-            for (int ty = 0; ty <= (int)M_GLTFPBR; ty++) {
-                const int n = lane_count(__builtin_amdgcn_ballot_w64(mt == ty));
-                if (n > bestn) bestn = n, best = ty;
-            }
-            defer = cand && mt != best;
-            if (defer) T.nh |= MAT_DEFERRED;
-        }
-        if (query_done<WIDE>(T) && !defer) {
+        if (query_done<WIDE>(T)) {
             bool alive = true;
             // no light query ever leaves the shading phase (FT_LINL), or none exists (FT_NOIL)
             const bool light = SAMPLER == 1 && !LINL && st.phase == PH_LIGHT;
