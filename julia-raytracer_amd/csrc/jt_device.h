@@ -11,9 +11,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#ifndef JT_STREAM_ITEMS
-#define JT_STREAM_ITEMS (1 << 24)  // automatic stream count: about this many (pixel, stream) items
-#endif
+// automatic stream count (jt_trace.hip stream_log2): at least JT_STREAMS_MIN streams and
+// JT_STREAM_ITEMS (pixel, stream) items, at most JT_STREAM_ITEMS_MAX items
+#define JT_STREAMS_MIN 16
+#define JT_STREAM_ITEMS (1LL << 22)
+#define JT_STREAM_ITEMS_MAX (1LL << 27)
 #ifndef JT_AUTO_WIDE_MIN_STACK
 #define JT_AUTO_WIDE_MIN_STACK 32  // JT_TRAVERSAL_AUTO: wide records for HBM-mode scenes deeper than this
 #endif

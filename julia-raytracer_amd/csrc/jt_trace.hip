@@ -429,14 +429,21 @@ int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_wo
 constexpr size_t SCHED_BYTES = (size_t)NBANDS * BAND_STRIDE * 4;
 
 // Sample streams per pixel (DESIGN.md §2 "Sample streams"), fixed at jt_create: 1 for the
-// reference's default one-sample batches (its single running mean), else the largest power of
-// two <= min(batch, JT_MAX_STREAMS) that keeps (pixels traced) x streams <= JT_STREAM_ITEMS:
-// enough independent (pixel, stream) items to fill the device with a short tail even when a
-// context traces only a tile share of the image, and stream means of at most JT_STREAM_ITEMS x
-// 48 B. The option "streams" (a power of two <= JT_MAX_STREAMS) overrides.
+// reference's default one-sample batches (its single running mean); otherwise at least 16 (a
+// stream item is then at most a sixteenth of a batch's samples: the launch ends on short items)
+// and enough for 2^22 (pixel, stream) items (a context tracing few pixels — a tile share, a small
+// image — still fills the GPU), at most 64, the batch, and 2^27 items of stream means (6.4 GB).
+// Measured (gpurun_out/r05i, r05j): bathroom1 1024 spp 8 -> 16 streams +0.8 %, features2 512 spp
+// +2 %, ecosys 64 spp 2 -> 16 +2.6 %, its 1/8 share (512 spp) +3.7 %; a 1/8 tile share of the
+// headline 32 streams 9265, 64 streams 9794 Mrays/s. The option "streams" overrides.
 int stream_log2(long long pixels, int batch) {
+    if (batch <= 1) return 0;
+    long long want = JT_STREAMS_MIN;
+    while (pixels * want < JT_STREAM_ITEMS) want *= 2;
     int lk = 0;
-    while (lk < 6 && (2 << lk) <= batch && (2 << lk) <= JT_MAX_STREAMS && pixels * (2LL << lk) <= JT_STREAM_ITEMS) lk++;
+    while (lk < 6 && (2LL << lk) <= want && (2 << lk) <= batch && (2 << lk) <= JT_MAX_STREAMS &&
+           pixels * (2LL << lk) <= JT_STREAM_ITEMS_MAX)
+        lk++;
     return lk;
 }
 
