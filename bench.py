@@ -405,7 +405,7 @@ def main():
                         hbm_frac=round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5))
             roof["binding"] = {k: d[k] for k in ("valu_issue_frac", "lane_util", "fp32_lane_frac", "td_busy_frac",
                                                  "td_unstalled_frac", "td_tc_stall_frac_of_busy", "l2_hit_rate",
-                                                 "vmem_mix_frac", "clock_ghz") if k in d}
+                                                 "vmem_mix_frac", "vmem_mix_frac_resident", "clock_ghz") if k in d}
             roof["binding"]["write_bytes_per_launch"] = int(d["write_bytes"])
             roof["binding"]["profiled_launch_ms"] = round(rec["duration_ns"] / 1e6, 3)
         alg_gbs = logical / avg_launch_s / 1e9

@@ -1430,12 +1430,6 @@ __host__ __device__ __forceinline__ int launch_tiles(const DParams& P) {
 #ifndef JT_ITEM_FIRST_POP
 #define JT_ITEM_FIRST_POP 2
 #endif
-// JT_START_IN_SHADE: a stream's next sample starts in the shading phase that finished the previous
-// one (camera ray there, the query start shared with the lanes continuing a path) instead of at the
-// top of the next iteration
-#ifndef JT_START_IN_SHADE
-#define JT_START_IN_SHADE 0
-#endif
 template <bool WIDE, int F>
 __host__ __device__ constexpr bool item_first_pop() {
     return JT_ITEM_FIRST_POP == 1 || (JT_ITEM_FIRST_POP == 2 && !WIDE && !ft_none(F));
@@ -1769,15 +1763,6 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                         A.part_nrm[o] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
                     }
                     item = ITEM_NONE;
-                } else if (JT_START_IN_SHADE) {
-                    // the stream's next sample starts here: its camera ray, then the same query
-                    // start as the lanes continuing a path (one converged query_start, not two)
-                    const int ns = sample + kstr;
-                    acc_i[11 * BLOCK] = ns;
-                    if (!ft_none(F)) acc[12 * BLOCK] = stream_weight(P, ns);
-                    const int pixel = item_pixel(item, P, tiles_x);
-                    start_path<F>(P, pixel % P.width, pixel / P.width, pixel, ns, st);
-                    alive = true;
                 } else {
                     acc_i[11 * BLOCK] = sample + kstr;  // started at the top of the next iteration
                     next_sample = true;

@@ -20,6 +20,10 @@ actually binds, computed from PMC counters the same way for every workload:
   vmem_mix_frac   = vmem_rd_gips / VMEM_MIX_PEAK_GIPS[traversal]   (the ceiling for the traversal's
                     own node records, scripts/td_mix_bench.hip: 64-B wide records 40.6 G/s, 16-B
                     binary node rows 34.7 G/s; profiles/r04_tdmix/)
+  vmem_mix_frac_resident = vmem_rd_gips / VMEM_MIX_PEAK_GIPS_RESIDENT[traversal]   (the same ceiling
+                    measured at the kernels' own residency: 4 workgroups of 4 waves per CU, 24 of 64
+                    lanes active; td_mix_bench 4 24, profiles/r05_tdmix/: 64-B records 41.85 G/s —
+                    as at full occupancy, so that frac is not lost occupancy — 16-B rows 22.38)
   td_unstalled_frac = td_busy_frac * (1 - TD_TC_STALL_sum / TD_TD_BUSY_sum)   (cycles the TD moves
                     data rather than waits on the cache for it; agrees with vmem_mix_frac)
 
@@ -53,6 +57,8 @@ VMEM_PEAK_GIPS = 2195.0 / 64
 # 1-25 % slower): the wide order's 64-B records are four dwordx4 of one record (40.60 G wave-instr/s),
 # the binary orders' 16-B node rows one dwordx4 (34.71)
 VMEM_MIX_PEAK_GIPS = {"wide": 40.60, "near": 34.71, "reference": 34.71}
+# at the HBM-mode kernels' residency (4 workgroups per CU, 24 active lanes; L2-resident set)
+VMEM_MIX_PEAK_GIPS_RESIDENT = {"wide": 41.85, "near": 22.38, "reference": 22.38}
 
 
 def record_traversal(rec):
@@ -180,6 +186,7 @@ def derive(rec):
             out["vmem_rd_gips"] = pmc["SQ_INSTS_VMEM_RD"] / pd / 1e9
             out["vmem_frac"] = out["vmem_rd_gips"] / VMEM_PEAK_GIPS
             out["vmem_mix_frac"] = out["vmem_rd_gips"] / VMEM_MIX_PEAK_GIPS[record_traversal(rec)]
+            out["vmem_mix_frac_resident"] = out["vmem_rd_gips"] / VMEM_MIX_PEAK_GIPS_RESIDENT[record_traversal(rec)]
         if "td_busy_frac" in out and "td_tc_stall_frac_of_busy" in out:
             out["td_unstalled_frac"] = out["td_busy_frac"] * (1.0 - out["td_tc_stall_frac_of_busy"])
     return {k: round(v, 6) for k, v in out.items()}
