@@ -486,12 +486,18 @@ __device__ __forceinline__ void query_start(const DScene& S, Trav& T, v3 o, v3 d
     else query_begin(S, T, o, d, inst < 0 ? ((T_TLAS << 30) | SNAP_NONE) : ((T_INST << 30) | SNAP_NONE | (unsigned)inst), stack, rerun);
 }
 // a finished near-first query that saw an exact-t tie: run it again in the reference's child order
-// (the same world ray; inst >= 0: the intersect_instance_bvh of that instance). Returns whether
-// the lane re-runs (its query is then not done).
+// (the same world ray (o, d): every query is started on its path's (st.o, st.d), which do not
+// change until its hit is consumed — so T.wo/T.wd stay dead in kernels without instance
+// transforms; inst >= 0: the intersect_instance_bvh of that instance). Returns whether the lane
+// re-runs (its query is then not done).
+// An instance query of a one-leaf BLAS (INST_LEAF_ROOT) tests its leaf's primitives in the same
+// order in every child order, so it is never re-run (the oracle's instance_query: the same rule).
+constexpr int INST_LEAF_ROOT = 2;
 template <bool WIDE>
-__device__ __forceinline__ bool rerun_tie(const DScene& S, Trav& T, int inst, int* stack) {
+__device__ __forceinline__ bool rerun_tie(const DScene& S, Trav& T, v3 o, v3 d, int inst, int* stack) {
     if (!JT_TIE_RERUN || (T.nh & (TIE_SEEN | REF_RERUN)) != TIE_SEEN || S.order_flip == 0) return false;
-    query_start<WIDE>(S, T, T.wo, T.wd, inst, stack, REF_RERUN);
+    if (inst >= 0 && (S.inst_blas[inst].y & INST_LEAF_ROOT)) return false;
+    query_start<WIDE>(S, T, o, d, inst, stack, REF_RERUN);
     return true;
 }
 
@@ -602,8 +608,8 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
     unsigned type = e >> 30, idx = e & IDX_MASK;
     if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
         if (COUNT) cnt.instances++;
-        const int4 ib = S.inst_blas[idx];  // blas_root, identity, kind, shape (one load: x, y adjacent)
-        if (!XF || ib.y) {
+        const int4 ib = S.inst_blas[idx];  // blas_root, identity | leaf root, kind, shape (one load: x, y adjacent)
+        if (!XF || (ib.y & 1)) {
             // inverse(identity) is exactly the identity: transform_ray returns the ray bit for bit
             if (XF && T.inst_space) world_ray(S, T);
         } else {
@@ -799,8 +805,8 @@ __device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* st
         const unsigned inst = w & W_START, n1 = (w >> 28) & 3u;
         if (n1) st_push<RING, OVF>(S, T, stack, pixel, W_LEAF | (n1 - 1u) << 24 | (inst + 1u));
         if (COUNT) cnt.instances++;
-        const int4 ib = S.inst_blas[inst];  // wide BLAS root record, identity, kind, shape
-        if (!XF || ib.y) {
+        const int4 ib = S.inst_blas[inst];  // wide BLAS root record, identity | leaf root, kind, shape
+        if (!XF || (ib.y & 1)) {
             if (XF && T.inst_space) world_ray(S, T);
         } else {
             const DInstTrav it = S.inst_trav[inst];
@@ -1100,10 +1106,7 @@ __device__ __forceinline__ bool light_chain(const DScene& S, const DParams& P, P
         query_start<WIDE>(S, T, st.o, st.d, inst, stack);
         node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);  // instance + its one-leaf root
         while (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-        if (rerun_tie<WIDE>(S, T, inst, stack)) {  // an exact-t tie: the reference's order decides
-            node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);
-            while (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-        }
+        // (no tie re-run: a one-leaf BLAS has no child order, INST_LEAF_ROOT)
         if (light_hit<F>(S, P, st, query_hit(T))) return true;
     } while (st.phase == PH_LIGHT);
     return false;
@@ -1616,7 +1619,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 const int nl = lane_count(__builtin_amdgcn_ballot_w64(wantl));
                 if (nl > 0 && (nl >= P.light_lanes || nb == 0)) {
                     bool c_lq = false, c_ray = false;
-                    if (wantl && rerun_tie<WIDE>(S, T, S.lights[st.li].instance, stack)) {
+                    if (wantl && rerun_tie<WIDE>(S, T, st.o, st.d, S.lights[st.li].instance, stack)) {
                         // an exact-t tie: the query runs again in the reference's order
                     } else if (wantl) {
                         if (light_hit<F>(S, P, st, query_hit(T))) {
@@ -1698,7 +1701,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
             const bool tie = query_done<WIDE>(T) && (T.nh & (TIE_SEEN | REF_RERUN)) == TIE_SEEN &&
                              !(LSTEP && st.phase == PH_FINISH);
             if (S.order_flip && __builtin_amdgcn_ballot_w64(tie))
-                if (tie) rerun_tie<WIDE>(S, T, SAMPLER == 1 && !LINL && st.phase == PH_LIGHT ? S.lights[st.li].instance : -1, stack);
+                if (tie) rerun_tie<WIDE>(S, T, st.o, st.d, SAMPLER == 1 && !LINL && st.phase == PH_LIGHT ? S.lights[st.li].instance : -1, stack);
         }
         bool c_path = false, c_lq = false, c_ray = false;
         unsigned n_inl = 0;

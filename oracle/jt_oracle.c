@@ -759,7 +759,9 @@ static scene_isec instance_query(const ctx_t* c, int inst_id, ray3 ray, scratch_
     sc->cnt.light_queries++;
     sc->tie = 0;
     scene_isec r = wide ? intersect_instance_wide(c, inst_id, ray, sc, near) : intersect_instance_bvh(c, inst_id, ray, sc, near);
-    if (near && sc->tie)
+    /* a one-leaf shape BVH tests its leaf in the same order in every child order: no re-run */
+    const jt_bvh_tree* bt = &c->bvh->blas[c->scene->instances[inst_id].shape];
+    if (near && sc->tie && bt->nnodes > 0 && bt->nodes[0].internal)
         r = wide ? intersect_instance_wide(c, inst_id, ray, sc, 0) : intersect_instance_bvh(c, inst_id, ray, sc, 0);
     return r;
 }
