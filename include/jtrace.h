@@ -79,7 +79,8 @@ typedef enum jt_sampler { JT_SAMPLER_PATH = 1, JT_SAMPLER_NAIVE = 2 } jt_sampler
  *   are visited (tmax shrinks sooner). Among hits at exactly equal t the reference's later-tested
  *   one wins (src/geometry.jl:226, t > tmax rejects), which depends on the order: a near-first
  *   query that accepts a hit at exactly its current tmax is run again in the reference's child
- *   order and reports that hit. The closest hit then differs from the reference's only where the
+ *   order and reports that hit (an intersect_instance_bvh of a one-leaf shape BVH has no child
+ *   order and is never re-run). The closest hit then differs from the reference's only where the
  *   slab test's rounding lets one order find a hit the other culls (measured: 2e-6 of bathroom1's
  *   paths, none on cornellbox, features2, ecosys).
  * JT_TRAVERSAL_WIDE: the reference's binary tree collapsed to 4-wide records (each internal node
