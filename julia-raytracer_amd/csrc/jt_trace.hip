@@ -126,6 +126,8 @@ __global__ __launch_bounds__(256) void combine_kernel(DParams P, DAccum A, DComb
     im = make_float4(im.x * w0, im.y * w0, im.z * w0, im.w * w0);
     al = make_float4(al.x * w0, al.y * w0, al.z * w0, 0.0f);
     nr = make_float4(nr.x * w0, nr.y * w0, nr.z * w0, 0.0f);
+    // unrolled: four streams' loads in flight per thread (the sums stay in stream order)
+#pragma unroll 4
     for (int s = 1; s < Cw.ns; s++) {
         const float w = Cw.w[s];
         const float4 a = A.part_img[s * np + pixel], b = A.part_alb[s * np + pixel], c = A.part_nrm[s * np + pixel];
