@@ -492,11 +492,11 @@ __device__ __forceinline__ void query_start(const DScene& S, Trav& T, v3 o, v3 d
 // re-runs (its query is then not done).
 // An instance query of a one-leaf BLAS (INST_LEAF_ROOT) tests its leaf's primitives in the same
 // order in every child order, so it is never re-run (the oracle's instance_query: the same rule).
-constexpr int INST_LEAF_ROOT = 2;
+constexpr int INST_LEAF_ROOT = 1 << 30;  // in the instance record's w (shape) word
 template <bool WIDE>
 __device__ __forceinline__ bool rerun_tie(const DScene& S, Trav& T, v3 o, v3 d, int inst, int* stack) {
     if (!JT_TIE_RERUN || (T.nh & (TIE_SEEN | REF_RERUN)) != TIE_SEEN || S.order_flip == 0) return false;
-    if (inst >= 0 && (S.inst_blas[inst].y & INST_LEAF_ROOT)) return false;
+    if (inst >= 0 && (S.inst_blas[inst].w & INST_LEAF_ROOT)) return false;
     query_start<WIDE>(S, T, o, d, inst, stack, REF_RERUN);
     return true;
 }
@@ -608,8 +608,8 @@ __device__ __forceinline__ void node_step(const DScene& S, Trav& T, int* stack, 
     unsigned type = e >> 30, idx = e & IDX_MASK;
     if (type == T_INST) {  // instance visit: inverse(frame, true) precomputed (src/bvh.jl:345,502)
         if (COUNT) cnt.instances++;
-        const int4 ib = S.inst_blas[idx];  // blas_root, identity | leaf root, kind, shape (one load: x, y adjacent)
-        if (!XF || (ib.y & 1)) {
+        const int4 ib = S.inst_blas[idx];  // blas_root, identity, kind, shape | leaf root (one load: x, y adjacent)
+        if (!XF || ib.y) {
             // inverse(identity) is exactly the identity: transform_ray returns the ray bit for bit
             if (XF && T.inst_space) world_ray(S, T);
         } else {
@@ -805,8 +805,8 @@ __device__ __forceinline__ void node_step_wide(const DScene& S, Trav& T, int* st
         const unsigned inst = w & W_START, n1 = (w >> 28) & 3u;
         if (n1) st_push<RING, OVF>(S, T, stack, pixel, W_LEAF | (n1 - 1u) << 24 | (inst + 1u));
         if (COUNT) cnt.instances++;
-        const int4 ib = S.inst_blas[inst];  // wide BLAS root record, identity | leaf root, kind, shape
-        if (!XF || (ib.y & 1)) {
+        const int4 ib = S.inst_blas[inst];  // wide BLAS root record, identity, kind, shape | leaf root
+        if (!XF || ib.y) {
             if (XF && T.inst_space) world_ray(S, T);
         } else {
             const DInstTrav it = S.inst_trav[inst];
@@ -1104,9 +1104,14 @@ __device__ __forceinline__ bool light_chain(const DScene& S, const DParams& P, P
         count_lq();
         const int inst = S.lights[st.li].instance;
         query_start<WIDE>(S, T, st.o, st.d, inst, stack);
-        node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);  // instance + its one-leaf root
-        while (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
-        // (no tie re-run: a one-leaf BLAS has no child order, INST_LEAF_ROOT)
+        // No tie re-run is needed here: a one-leaf BLAS has no child order (INST_LEAF_ROOT). The
+        // FT_MESH kernel (bathroom1) keeps the re-run loop anyway, never taken: its compiled
+        // layout is 4 % faster with it, features2's kernel 1.5 % slower (gpurun_out/r05v)
+        constexpr bool RERUN_LOOP = (F & ~FT_LINL) == (FT_TEX | FT_ATTR | FT_MAT | FT_OPAC | FT_XFORM);  // FT_MESH
+        do {
+            node_step_any<WIDE, RING, OVF, COUNT, NCACHE, F>(S, T, stack, pixel, cnt);  // instance + its one-leaf root
+            while (T.nprim > 0) prim_step<COUNT, F>(S, T, cnt);
+        } while (RERUN_LOOP && rerun_tie<WIDE>(S, T, st.o, st.d, inst, stack));
         if (light_hit<F>(S, P, st, query_hit(T))) return true;
     } while (st.phase == PH_LIGHT);
     return false;

@@ -861,13 +861,13 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         const float idm[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
         bool ident = true;
         for (int q = 0; q < 12; q++) ident = ident && iv[q] == idm[q];
-        // jtk::node_step reads x, y (z); the wide traversal's x is the BLAS's root record. y: bit 0
-        // the identity inverse, bit 1 (jtk::INST_LEAF_ROOT) a one-leaf BLAS: its
-        // intersect_instance_bvh tests the leaf's primitives in order whatever the child order, so
-        // an exact-t tie there needs no re-run in the reference's order (jtk::rerun_tie)
+        // jtk::node_step reads x, y (z); the wide traversal's x is the BLAS's root record; y the
+        // identity inverse; w the shape, with bit 30 (jtk::INST_LEAF_ROOT) set for a one-leaf BLAS:
+        // its intersect_instance_bvh tests the leaf's primitives in order whatever the child order,
+        // so an exact-t tie there needs no re-run in the reference's order (jtk::rerun_tie)
         const jt_bvh_tree& bt = bvh->blas[in.shape];
         const bool leaf_root = bt.nnodes > 0 && !bt.nodes[0].internal;
-        iblas[k] = make_int4(c->wide ? wroot[in.shape] : d.blas_root, (ident ? 1 : 0) | (leaf_root ? 2 : 0), d.kind, in.shape);
+        iblas[k] = make_int4(c->wide ? wroot[in.shape] : d.blas_root, ident ? 1 : 0, d.kind, in.shape | (leaf_root ? 1 << 30 : 0));
         if (!ident) c->feat |= FT_XFORM;
         ishade[k] = DInstShade{f4(fv[0], fv[1], fv[2], fv[3]), f4(fv[4], fv[5], fv[6], fv[7]), f4(fv[8], fv[9], fv[10], fv[11]),
                                in.material, in.shape, scene->materials[in.material].type,
