@@ -387,6 +387,13 @@ struct Trav {
 // queries, none on cornellbox), so the hot path only records them (at an accepted hit), and the
 // re-run runs where the query's hit is consumed (rerun_tie). A re-run is the same query: it is
 // not counted as a ray or light query again; its node and primitive work is counted (COUNT=1).
+#ifndef JT_BAND_STRIP
+// tile rows per strip of a band's unit order (1: row-major). Measured against row-major
+// (gpurun_out/r05st, r05st2, two runs each): 16 rows cornellbox +2.0 %, features2 +1.1 %, ecosys
+// +1.1 %; 8 rows cornellbox +1.3 %, features2 +1.4 %, ecosys +1.1 %, bathroom1 +0.4 %; 4 rows
+// and 32 rows in between
+#define JT_BAND_STRIP 16
+#endif
 #ifndef JT_TIE_RERUN
 #define JT_TIE_RERUN 1  // 0: ties resolve in the near-first order's own sequence (A/B runs only)
 #endif
@@ -1529,7 +1536,14 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
             if (!needm || drained) break;
             if (bnext >= 64) {  // the next unit of this XCD's band, or of the next band
                 const int band = (int)((xcc + (unsigned)band_k) & (NBANDS - 1));
-                const int bt0 = band * tiles / NBANDS, bn = (band + 1) * tiles / NBANDS - bt0;
+                // JT_BAND_STRIP > 1 (whole images; tile shares keep the plain split): bands of whole
+                // tile rows, each walked in strips of that many rows, column by column, so the tiles
+                // in flight on an XCD form a compact block (their rays share nodes and texels in L2)
+                constexpr int STRIP = JT_BAND_STRIP;
+                const bool strips = STRIP > 1 && P.tile_stride == 1;
+                const int tiles_y = (P.height + 7) / 8;
+                const int bt0 = strips ? band * tiles_y / NBANDS * tiles_x : band * tiles / NBANDS;
+                const int bn = strips ? (band + 1) * tiles_y / NBANDS * tiles_x - bt0 : (band + 1) * tiles / NBANDS - bt0;
                 unsigned unit = 0;
                 if (lane == 0) unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
                 unit = __builtin_amdgcn_readfirstlane(unit);
@@ -1538,7 +1552,14 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                     continue;
                 }
                 uq = (int)(unit % (unsigned)nq);  // tile-major (NBANDS above)
-                ut = (bt0 + (int)(unit / (unsigned)nq)) * P.tile_stride + P.tile_offset;
+                const int tu = (int)(unit / (unsigned)nq);
+                int tile = bt0 + tu;
+                if (strips) {
+                    const int rows = bn / tiles_x, sidx = tu / (STRIP * tiles_x);
+                    const int v = tu - sidx * STRIP * tiles_x, h = rows - sidx * STRIP < STRIP ? rows - sidx * STRIP : STRIP;
+                    tile = bt0 + (sidx * STRIP + v % h) * tiles_x + v / h;
+                }
+                ut = tile * P.tile_stride + P.tile_offset;
                 bnext = 0;
             }
             const int nneed = lane_count(needm), take = nneed < 64 - bnext ? nneed : 64 - bnext;
