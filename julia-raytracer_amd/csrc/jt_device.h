@@ -11,9 +11,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// automatic stream count (jt_trace.hip stream_log2): at least JT_STREAMS_MIN streams and
-// JT_STREAM_ITEMS (pixel, stream) items, at most JT_STREAM_ITEMS_MAX items
+// automatic stream count (jt_trace.hip stream_log2): at least JT_STREAMS_MIN streams —
+// JT_STREAMS_WIDE for a batch of at least two samples per such stream — and JT_STREAM_ITEMS
+// (pixel, stream) items, at most JT_STREAM_ITEMS_MAX items
 #define JT_STREAMS_MIN 16
+#define JT_STREAMS_WIDE 32
 #define JT_STREAM_ITEMS (1LL << 22)
 #define JT_STREAM_ITEMS_MAX (1LL << 27)
 #ifndef JT_AUTO_WIDE_MIN_STACK

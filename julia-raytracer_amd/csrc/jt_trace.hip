@@ -440,7 +440,7 @@ constexpr size_t SCHED_BYTES = (size_t)NBANDS * BAND_STRIDE * 4;
 // headline 32 streams 9265, 64 streams 9794 Mrays/s. The option "streams" overrides.
 int stream_log2(long long pixels, int batch) {
     if (batch <= 1) return 0;
-    long long want = JT_STREAMS_MIN;
+    long long want = batch >= 2 * JT_STREAMS_WIDE ? JT_STREAMS_WIDE : JT_STREAMS_MIN;
     while (pixels * want < JT_STREAM_ITEMS) want *= 2;
     int lk = 0;
     while (lk < 6 && (2LL << lk) <= want && (2 << lk) <= batch && (2 << lk) <= JT_MAX_STREAMS &&

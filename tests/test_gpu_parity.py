@@ -255,9 +255,9 @@ def test_sample_streams_match_the_oracle(gpu, abi, lib, oracle, cornell_abi, sam
 
 
 def test_stream_count_rule(gpu, abi, lib, cornell_abi, options):
-    """jt_get_streams: 1 at --batch 1, else the smallest power of two >= 16 with (pixels traced)
-    x k >= 2^22, capped at min(batch, 64) and (pixels) x k <= 2^27 (include/jtrace.h); a tile
-    share counts its own pixels."""
+    """jt_get_streams: 1 at --batch 1, else the smallest power of two >= 16 (>= 32 from a batch
+    of 64) with (pixels traced) x k >= 2^22, capped at min(batch, 64) and (pixels) x k <= 2^27
+    (include/jtrace.h); a tile share counts its own pixels."""
     from jtrace import trace
     bvh = trace.make_scene_bvh(cornell_abi, False, lib)
     lights = trace.make_trace_lights(cornell_abi, lib)
@@ -265,7 +265,7 @@ def test_stream_count_rule(gpu, abi, lib, cornell_abi, options):
     def rule(px, batch):
         if batch <= 1:
             return 1
-        want = 16
+        want = 32 if batch >= 64 else 16
         while px * want < 1 << 22:
             want *= 2
         k = 1
@@ -273,8 +273,9 @@ def test_stream_count_rule(gpu, abi, lib, cornell_abi, options):
             k *= 2
         return k
 
-    expect = {(1280, 720, 256, 1): 16, (1280, 720, 1, 1): 1, (256, 256, 16, 1): 16, (1920, 1080, 1024, 1): 16,
-              (3840, 2160, 4096, 1): 16, (1280, 720, 256, 8): 64, (64, 64, 5, 1): 4, (7680, 4320, 64, 1): 4}
+    expect = {(1280, 720, 256, 1): 32, (1280, 720, 32, 1): 16, (1280, 720, 1, 1): 1, (256, 256, 16, 1): 16,
+              (1920, 1080, 1024, 1): 32, (3840, 2160, 4096, 1): 16, (1280, 720, 256, 8): 64, (64, 64, 5, 1): 4,
+              (7680, 4320, 64, 1): 4}
     for (w, h, batch, share), k in expect.items():
         options("tile_share", f"{share},0" if share > 1 else None)
         st = trace.make_trace_state(cornell_abi, bvh, lights, make_params(abi, width=w, height=h, samples=batch,
