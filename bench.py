@@ -170,32 +170,34 @@ def main():
     scene = sceneio.load_scene(args.scene, missing="drop")  # configs 3-5: the checkout lacks a few files
     sa = abi.SceneABI(scene)
     t_load = time.perf_counter()
-    params = Params(scene=args.scene, samples=args.spp, sampler=2 if args.sampler == "naive" else 1,
-                    width=args.width, height=args.height, device=dev, batch=args.spp, traversal=args.traversal)
-    jp = abi.make_params(params, 0)
-    bvh = trace.make_scene_bvh(sa, args.highqualitybvh, lib)
-    t_bvh = time.perf_counter()
-    lights = trace.make_trace_lights(sa, lib)
-    t_lights = time.perf_counter()
-    state = trace.make_trace_state(sa, bvh, lights, jp, lib)
-    t_create = time.perf_counter()
-    ttfp = {"load_s": round(t_load - t_0, 3), "bvh_s": round(t_bvh - t_load, 3),
-            "lights_s": round(t_lights - t_bvh, 3), "upload_s": round(t_create - t_lights, 3),
-            "total_s": round(t_create - t_0, 3)}
-    W, H, S = state.width, state.height, args.spp
     from jtrace.parallel import (PipelinedReduce, compare_signature, image_signature, load_signature,
                                  save_signature, split_plan)
+    S = args.spp
     # this rank's share: 1/G of the 8x8 tiles (G = --tile-groups) x a contiguous
     # 1/(N/G) of the samples; G = 1 is the pure sample split
     groups = args.tile_groups if args.tile_groups > 0 else 1
     # --as-rank-of N (N=1 runs only): trace rank 0's share of an N-rank run, to measure it on one GPU
     plan_world, plan_rank = (args.as_rank_of, 0) if (args.as_rank_of and world == 1) else (world, rank)
     share, s0, s1 = split_plan(plan_world, plan_rank, S, groups)
-    if share is not None:  # the context must be created with the option: recreate it
-        state.close()
+    # the rank's trace_samples batch is its own share of the samples (one launch per step; the
+    # library sizes its sample streams by it, jt_get_streams)
+    params = Params(scene=args.scene, samples=S, sampler=2 if args.sampler == "naive" else 1,
+                    width=args.width, height=args.height, device=dev, batch=s1 - s0, traversal=args.traversal)
+    jp = abi.make_params(params, 0)
+    bvh = trace.make_scene_bvh(sa, args.highqualitybvh, lib)
+    t_bvh = time.perf_counter()
+    lights = trace.make_trace_lights(sa, lib)
+    t_lights = time.perf_counter()
+    if share is not None:  # a tile share: the context is created with the option
         abi.set_option(lib, "tile_share", share)
-        state = trace.make_trace_state(sa, bvh, lights, jp, lib)
+    state = trace.make_trace_state(sa, bvh, lights, jp, lib)
+    if share is not None:
         abi.set_option(lib, "tile_share", None)
+    t_create = time.perf_counter()
+    ttfp = {"load_s": round(t_load - t_0, 3), "bvh_s": round(t_bvh - t_load, 3),
+            "lights_s": round(t_lights - t_bvh, 3), "upload_s": round(t_create - t_lights, 3),
+            "total_s": round(t_create - t_0, 3)}
+    W, H = state.width, state.height
 
     traversal = state.traversal  # "auto" resolved by the library: wide for deep HBM-mode scenes, near otherwise
     workload = f"{Path(args.scene).stem} {args.sampler} {W}x{H} {s1 - s0} samples/launch" + \
@@ -306,7 +308,8 @@ def main():
     # Reference-order leg (rank 0, N=1): the same workload with the reference's far-child-first
     # order (src/bvh.jl:331-341, SURVEY Appendix B item 9: performance only), timed the same way,
     # and the fraction of pixels whose final running mean differs from the near-first image (only
-    # exact-t ties can resolve differently)
+    # hits the slab test's rounding lets one order find and the other cull; exact-t ties re-run in
+    # the reference's order)
     ref_order = None
     if rank == 0 and world == 1 and not partial and args.traversal != "reference" and not args.no_reference_order:
         img_near = state.get_image()
