@@ -1536,14 +1536,17 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
             if (!needm || drained) break;
             if (bnext >= 64) {  // the next unit of this XCD's band, or of the next band
                 const int band = (int)((xcc + (unsigned)band_k) & (NBANDS - 1));
-                // JT_BAND_STRIP > 1 (whole images; tile shares keep the plain split): bands of whole
-                // tile rows, each walked in strips of that many rows, column by column, so the tiles
-                // in flight on an XCD form a compact block (their rays share nodes and texels in L2)
+                // JT_BAND_STRIP > 1: bands of whole tile rows, each walked in strips of that many
+                // rows, column by column, so the tiles in flight on an XCD form a compact block
+                // (their rays share nodes and texels in L2).
+                // A tile share (tile_stride D) whose D divides the tile columns is a grid of
+                // tiles_x / D columns in launch-tile numbering and is walked the same way.
                 constexpr int STRIP = JT_BAND_STRIP;
-                const bool strips = STRIP > 1 && P.tile_stride == 1;
+                const int gx = tiles_x % P.tile_stride == 0 ? tiles_x / P.tile_stride : 0;
+                const bool strips = STRIP > 1 && gx > 0;
                 const int tiles_y = (P.height + 7) / 8;
-                const int bt0 = strips ? band * tiles_y / NBANDS * tiles_x : band * tiles / NBANDS;
-                const int bn = strips ? (band + 1) * tiles_y / NBANDS * tiles_x - bt0 : (band + 1) * tiles / NBANDS - bt0;
+                const int bt0 = strips ? band * tiles_y / NBANDS * gx : band * tiles / NBANDS;
+                const int bn = strips ? (band + 1) * tiles_y / NBANDS * gx - bt0 : (band + 1) * tiles / NBANDS - bt0;
                 unsigned unit = 0;
                 if (lane == 0) unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
                 unit = __builtin_amdgcn_readfirstlane(unit);
@@ -1555,9 +1558,9 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 const int tu = (int)(unit / (unsigned)nq);
                 int tile = bt0 + tu;
                 if (strips) {
-                    const int rows = bn / tiles_x, sidx = tu / (STRIP * tiles_x);
-                    const int v = tu - sidx * STRIP * tiles_x, h = rows - sidx * STRIP < STRIP ? rows - sidx * STRIP : STRIP;
-                    tile = bt0 + (sidx * STRIP + v % h) * tiles_x + v / h;
+                    const int rows = bn / gx, sidx = tu / (STRIP * gx);
+                    const int v = tu - sidx * STRIP * gx, h = rows - sidx * STRIP < STRIP ? rows - sidx * STRIP : STRIP;
+                    tile = bt0 + (sidx * STRIP + v % h) * gx + v / h;
                 }
                 ut = tile * P.tile_stride + P.tile_offset;
                 bnext = 0;
