@@ -345,7 +345,8 @@ int jt_trace_samples(jt_ctx* ctx);
 int jt_trace_range(jt_ctx* ctx, int32_t sample_begin, int32_t sample_end);
 /* The context's sample streams per pixel k (jt_trace_range). Chosen by jt_create: 1 when
  * params->batch is 1 (the reference's default); otherwise the smallest power of two k >= 16
- * (>= 32 when the batch is at least 64) with (pixels the context traces) * k >= 2^22, reduced to
+ * (>= 32 for a scene too large for LDS mode and a batch of at least 64; jt_describe reports the
+ * mode) with (pixels the context traces) * k >= 2^22, reduced to
  * at most 64, the batch, and (pixels) * k <= 2^27 (at least 1); or the "streams" option. */
 int jt_get_streams(const jt_ctx* ctx, int32_t* streams);
 int jt_get_samples(const jt_ctx* ctx, int32_t* samples);

@@ -437,10 +437,13 @@ constexpr size_t SCHED_BYTES = (size_t)NBANDS * BAND_STRIDE * 4;
 // image — still fills the GPU), at most 64, the batch, and 2^27 items of stream means (6.4 GB).
 // Measured (gpurun_out/r05i, r05j): bathroom1 1024 spp 8 -> 16 streams +0.8 %, features2 512 spp
 // +2 %, ecosys 64 spp 2 -> 16 +2.6 %, its 1/8 share (512 spp) +3.7 %; a 1/8 tile share of the
-// headline 32 streams 9265, 64 streams 9794 Mrays/s. The option "streams" overrides.
-int stream_log2(long long pixels, int batch) {
+// headline 32 streams 9265, 64 streams 9794 Mrays/s. A context whose scene runs from HBM starts
+// from 32 streams when the batch gives each at least two samples (gpurun_out/r05sk, r05sk2:
+// features2 +0.6 %, bathroom1 +0.5 %); an LDS-mode one (cornellbox) keeps 16: 32 gained it 1.0 %
+// but doubled its stream-mean stores (1.9 GB per launch). The option "streams" overrides.
+int stream_log2(long long pixels, int batch, bool hbm_scene) {
     if (batch <= 1) return 0;
-    long long want = batch >= 2 * JT_STREAMS_WIDE ? JT_STREAMS_WIDE : JT_STREAMS_MIN;
+    long long want = hbm_scene && batch >= 2 * JT_STREAMS_WIDE ? JT_STREAMS_WIDE : JT_STREAMS_MIN;
     while (pixels * want < JT_STREAM_ITEMS) want *= 2;
     int lk = 0;
     while (lk < 6 && (2LL << lk) <= want && (2 << lk) <= batch && (2 << lk) <= JT_MAX_STREAMS &&
@@ -1173,7 +1176,7 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         }
     }
     // sample streams: from the pixels this context traces (a tile share traces 1/stride of them)
-    c->lk = stream_log2(((long long)W * H + P.tile_stride - 1) / P.tile_stride, std::max(1, params->batch));
+    c->lk = stream_log2(((long long)W * H + P.tile_stride - 1) / P.tile_stride, std::max(1, params->batch), S.blob_n16 == 0);
     if (const char* ks = opt("streams")) {
         const int k = std::atoi(ks);
         if (k < 1 || k > JT_MAX_STREAMS || (k & (k - 1)) != 0)

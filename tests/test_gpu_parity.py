@@ -256,16 +256,17 @@ def test_sample_streams_match_the_oracle(gpu, abi, lib, oracle, cornell_abi, sam
 
 def test_stream_count_rule(gpu, abi, lib, cornell_abi, options):
     """jt_get_streams: 1 at --batch 1, else the smallest power of two >= 16 (>= 32 from a batch
-    of 64) with (pixels traced) x k >= 2^22, capped at min(batch, 64) and (pixels) x k <= 2^27
-    (include/jtrace.h); a tile share counts its own pixels."""
+    of 64 in HBM mode) with (pixels traced) x k >= 2^22, capped at min(batch, 64) and (pixels) x
+    k <= 2^27 (include/jtrace.h); a tile share counts its own pixels. Cornellbox runs in LDS mode;
+    the `lds_scene=0` option puts it in HBM mode."""
     from jtrace import trace
     bvh = trace.make_scene_bvh(cornell_abi, False, lib)
     lights = trace.make_trace_lights(cornell_abi, lib)
 
-    def rule(px, batch):
+    def rule(px, batch, hbm):
         if batch <= 1:
             return 1
-        want = 32 if batch >= 64 else 16
+        want = 32 if hbm and batch >= 64 else 16
         while px * want < 1 << 22:
             want *= 2
         k = 1
@@ -273,16 +274,20 @@ def test_stream_count_rule(gpu, abi, lib, cornell_abi, options):
             k *= 2
         return k
 
-    expect = {(1280, 720, 256, 1): 32, (1280, 720, 32, 1): 16, (1280, 720, 1, 1): 1, (256, 256, 16, 1): 16,
-              (1920, 1080, 1024, 1): 32, (3840, 2160, 4096, 1): 16, (1280, 720, 256, 8): 64, (64, 64, 5, 1): 4,
-              (7680, 4320, 64, 1): 4}
-    for (w, h, batch, share), k in expect.items():
+    # (width, height, batch, tile share, HBM mode): streams
+    expect = {(1280, 720, 256, 1, 0): 16, (1280, 720, 256, 1, 1): 32, (1280, 720, 32, 1, 1): 16,
+              (1280, 720, 1, 1, 0): 1, (256, 256, 16, 1, 0): 16, (1920, 1080, 1024, 1, 1): 32,
+              (1920, 1080, 1024, 1, 0): 16, (3840, 2160, 4096, 1, 1): 16, (1280, 720, 256, 8, 0): 64,
+              (64, 64, 5, 1, 0): 4, (7680, 4320, 64, 1, 1): 4}
+    for (w, h, batch, share, hbm), k in expect.items():
         options("tile_share", f"{share},0" if share > 1 else None)
+        options("lds_scene", "0" if hbm else None)
         st = trace.make_trace_state(cornell_abi, bvh, lights, make_params(abi, width=w, height=h, samples=batch,
                                                                           batch=batch), lib)
+        assert ("mode=hbm" in st.describe()) == bool(hbm), st.describe()
         tiles = ((w + 7) // 8) * ((h + 7) // 8)
         px = w * h if share == 1 else -(-w * h // share)
-        assert st.streams == rule(px, batch) == k, (w, h, batch, share, st.streams, tiles)
+        assert st.streams == rule(px, batch, hbm) == k, (w, h, batch, share, hbm, st.streams, tiles)
         st.close()
 
 
