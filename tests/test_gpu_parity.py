@@ -291,6 +291,35 @@ def test_stream_count_rule(gpu, abi, lib, cornell_abi, options):
         st.close()
 
 
+@pytest.mark.parametrize("w,h,batch,share", [(13, 7, 4, 1), (203, 77, 8, 1), (40, 330, 4, 1), (200, 72, 4, 5),
+                                               (200, 72, 4, 3)])
+def test_band_strip_order_covers_every_pixel_once(gpu, abi, lib, oracle, cornell_abi, w, h, batch, share, options):
+    """The work-unit order (XCD bands of whole tile rows walked in 16-row strips, column by
+    column; a tile share whose stride divides the tile columns walks its own grid the same way,
+    others the plain split) hands out every (pixel, stream) item exactly once: odd sizes with
+    partial edge tiles, fewer tile rows than bands, and tile shares on and off the strip path,
+    against the oracle (the share's pixels against the oracle's full image; paths exact)."""
+    options("tile_share", f"{share},1" if share > 1 else None)
+    params = make_params(abi, width=w, height=h, samples=batch, batch=batch)
+    g, o = _render_both(abi, lib, oracle, cornell_abi, params, 0, batch)
+    tiles_x = (w + 7) // 8
+    if share > 1:  # the share's pixels: tiles 1, 1 + share, ...; the oracle traced every pixel
+        ty, tx = np.divmod(np.arange(tiles_x * ((h + 7) // 8)), tiles_x)
+        mine = (ty * tiles_x + tx) % share == 1
+        mask = np.zeros((h, w), bool)
+        for t in np.nonzero(mine)[0]:
+            mask[ty[t] * 8:ty[t] * 8 + 8, tx[t] * 8:tx[t] * 8 + 8] = True
+        assert np.all(g[0][~mask] == 0), "a pixel outside the share was traced"
+        assert g[4]["paths"] == int(mask.sum()) * batch
+    else:
+        mask = np.ones((h, w), bool)
+        assert g[4]["paths"] == o[4]["paths"] == w * h * batch
+    same = np.all(g[0][mask] == o[0][mask], axis=-1)
+    print(w, h, batch, share, "pixels", int(mask.sum()), "bit-equal", float(same.mean()))
+    assert same.mean() >= 0.999  # the §8(c) bar; in practice every pixel
+    assert np.array_equal(g[3][mask], o[3][mask])
+
+
 def test_device_buffer_view_is_the_running_mean(gpu, abi, lib, cornell_abi):
     """bench.py's multi-GPU reduce reads the library's running-mean image in place through
     __cuda_array_interface__ (jt_get_device_buffers): that view must be exactly jt_get_image, and
