@@ -131,7 +131,7 @@ def main():
     ap.add_argument("--as-rank-of", type=int, default=0,
                     help="N=1: trace rank 0's share of an N-rank run (per-GPU rate and roofline of that share)")
     ap.add_argument("--write-signature", action="store_true",
-                    help="N=1: record this workload's image fingerprint in profiles/image_signatures.json")
+                    help="N=1: record this workload's image fingerprint in profiles/image_signatures.json (with --as-rank-of: rank 0's share image)")
     ap.add_argument("--print-workload", action="store_true",
                     help="print the workload key of this run's roofline record (scripts/gpu_measure.sh) and exit")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
@@ -285,18 +285,19 @@ def main():
     # Image check (rank 0, every N): block means of the final image — the RCCL-reduced one for
     # N > 1 — against the one-GPU signature committed for this workload (profiles/image_signatures.json,
     # jtrace/parallel.py): a wrong shard split, weight or reduce fails the run loudly
+    # (--as-rank-of N: rank 0's share image, against the signature of that share)
     image_check = None
     partial = world == 1 and plan_world > 1  # --as-rank-of: one rank's share only, not the image
-    if rank == 0 and partial:
-        image_check = {"ok": None, "why": f"--as-rank-of {plan_world}: rank 0's share only"}
-    elif rank == 0:
+    if rank == 0:
         img_final = (reduced[0].detach().cpu().numpy().reshape(H, W, 4) if world > 1 else state.get_image())
         sig = image_signature(img_final)
         sig_key = f"{Path(args.scene).stem} {args.sampler} {W}x{H}x{S}spp traversal={traversal}" + \
-            (" bvh=sah" if args.highqualitybvh else "")
+            (" bvh=sah" if args.highqualitybvh else "") + \
+            (f" rank 0 of {plan_world}" + (f" tiles 1/{groups}" if groups > 1 else "") if partial else "")
         ref_sig = load_signature(SIGNATURES, sig_key)
         if args.write_signature and world == 1:
-            save_signature(SIGNATURES, sig_key, sig, "one-GPU bench.py run, block means of the final image")
+            save_signature(SIGNATURES, sig_key, sig, "one-GPU bench.py --as-rank-of run, block means of rank 0's share image"
+                           if partial else "one-GPU bench.py run, block means of the final image")
             image_check = {"key": sig_key, "written": str(SIGNATURES.relative_to(ROOT))}
         elif ref_sig is not None:
             image_check = {"key": sig_key, **compare_signature(sig, ref_sig), "ranks_reduced": world}
