@@ -227,9 +227,9 @@ def test_inline_light_chains_bitwise_equal(gpu, abi, lib, options, name, lds):
         assert outs[0][2][k] == outs[1][2][k], k
 
 
-@pytest.mark.parametrize("name", ["bathroom1", "ecosys"])
-def test_hbm_scene_streams_match_the_oracle(gpu, abi, lib, oracle, options, name):
-    """The HBM-mode specialisations with the wide traversal and 32 sample streams (the automatic
+@pytest.mark.parametrize("name,order", [("bathroom1", "wide"), ("ecosys", "wide"), ("features2", "near")])
+def test_hbm_scene_streams_match_the_oracle(gpu, abi, lib, oracle, options, name, order):
+    """The HBM-mode specialisations in their auto traversal and 32 sample streams (the automatic
     count for features2/bathroom1 at their spp), in two calls whose second continues every
     stream's running mean from HBM, against the oracle's restatement of the same traversal,
     streams and combination: at the parity bar, hits and paths exact."""
@@ -237,11 +237,11 @@ def test_hbm_scene_streams_match_the_oracle(gpu, abi, lib, oracle, options, name
     sa = scene_abi(name)
     options("streams", "32")
     w, h, s = 120, 68, 40
-    p = make_params(abi, width=w, height=h, samples=s, batch=s, traversal="wide")
+    p = make_params(abi, width=w, height=h, samples=s, batch=s, traversal=order)
     bvh = trace.make_scene_bvh(sa, False, lib)
     lights = trace.make_trace_lights(sa, lib)
     st = trace.make_trace_state(sa, bvh, lights, p, lib)
-    assert st.streams == 32 and "mode=hbm" in st.describe() and "traversal=wide" in st.describe(), st.describe()
+    assert st.streams == 32 and "mode=hbm" in st.describe() and f"traversal={order}" in st.describe(), st.describe()
     st.trace_range(0, 24)
     st.trace_range(24, s)
     g = (st.get_image(), *st.get_aovs(), st.counters())
@@ -252,7 +252,7 @@ def test_hbm_scene_streams_match_the_oracle(gpu, abi, lib, oracle, options, name
     o = oracle.trace(sa, ob, ol, p, w, h, 24, s, streams=32, parts=parts, nthreads=8,
                      state=tuple(np.zeros(x.shape, x.dtype) for x in (g[0], g[1], g[2], g[3])))
     stats = compare_images(g[0], o[0])
-    print(name, "wide, 32 streams", stats, "gpu", g[4], "oracle", o[4])
+    print(name, order, "32 streams", stats, "gpu", g[4], "oracle", o[4])
     assert stats["frac_pix_rel_le_1e-3"] >= 0.999 and stats["image_mean_rel"] <= 1e-4, stats
     assert np.array_equal(g[3], o[3])
     for a, b in zip(g[1:3], o[1:3]):
