@@ -30,6 +30,10 @@ from jtrace.cli import DEFAULT_TRAVERSAL  # noqa: E402  (pure Python: no torch, 
 METRIC_BASE = "Mrays/s + wall-clock render time"  # BASELINE.json metric; the workload is appended
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SIGNATURES = ROOT / "profiles" / "image_signatures.json"  # one-GPU image fingerprints per workload
+# run-time options that change which samples are drawn (include/jtrace.h), hence the fingerprint;
+# the batch and the stream count only change the summation order (last bits), which the
+# fingerprint's tolerance absorbs, so every --batch checks against the same fingerprint
+RESULT_OPTIONS = ("env_alias",)
 
 
 def metric_name(scene: str, sampler: str, W: int, H: int, S: int) -> str:
@@ -120,6 +124,10 @@ def main():
                          "far-first order (src/bvh.jl:331-341)")
     ap.add_argument("--no-reference-order", action="store_true",
                     help="skip the reference-order comparison line (rank 0, N=1, --traversal near)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="trace_samples batch B (the reference's --batch, src/cli.jl:78-81; its default is 1): a step "
+                         "makes one call per B samples, as Jtrace.main does (src/jtrace.jl:83); 0 (the default): "
+                         "the rank's whole sample share in one call")
     ap.add_argument("--highqualitybvh", action="store_true",
                     help="the reference's SAH build (--highqualitybvh, src/bvh.jl:218-274) instead of split_middle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -179,10 +187,11 @@ def main():
     # --as-rank-of N (N=1 runs only): trace rank 0's share of an N-rank run, to measure it on one GPU
     plan_world, plan_rank = (args.as_rank_of, 0) if (args.as_rank_of and world == 1) else (world, rank)
     share, s0, s1 = split_plan(plan_world, plan_rank, S, groups)
-    # the rank's trace_samples batch is its own share of the samples (one launch per step; the
-    # library sizes its sample streams by it, jt_get_streams)
+    # the rank's trace_samples batch is its own share of the samples (one call per step; the
+    # library sizes its sample streams by it, jt_get_streams), or --batch B: one call per B samples
+    batch = args.batch if args.batch > 0 else s1 - s0
     params = Params(scene=args.scene, samples=S, sampler=2 if args.sampler == "naive" else 1,
-                    width=args.width, height=args.height, device=dev, batch=s1 - s0, traversal=args.traversal)
+                    width=args.width, height=args.height, device=dev, batch=batch, traversal=args.traversal)
     jp = abi.make_params(params, 0)
     bvh = trace.make_scene_bvh(sa, args.highqualitybvh, lib)
     t_bvh = time.perf_counter()
@@ -200,7 +209,8 @@ def main():
     W, H = state.width, state.height
 
     traversal = state.traversal  # "auto" resolved by the library: wide for deep HBM-mode scenes, near otherwise
-    workload = f"{Path(args.scene).stem} {args.sampler} {W}x{H} {s1 - s0} samples/launch" + \
+    workload = f"{Path(args.scene).stem} {args.sampler} {W}x{H} " + \
+        (f"{s1 - s0} samples/launch" if args.batch <= 0 else f"{s1 - s0} samples in calls of {batch}") + \
         (f" tiles 1/{groups}" if groups > 1 else "") + \
         ("" if traversal == "reference" else f" traversal={traversal}") + \
         (" bvh=sah" if args.highqualitybvh else "")
@@ -229,9 +239,18 @@ def main():
         red = PipelinedReduce(H * W * 4, s1 - s0, S, dist, device=img_t.device if backend == "nccl" else "cpu",
                               sync=torch.cuda.current_stream().synchronize)
 
+    full_range = s0 == 0 and s1 == S
+
     def step():
         state.reset()
-        state.trace_range(s0, s1)  # returns when the launch has finished (HIP event sync)
+        if args.batch <= 0:
+            state.trace_range(s0, s1)  # one call: returns when the launch has finished (HIP event sync)
+        elif full_range:  # Jtrace.main's loop (src/jtrace.jl:83-106): trace_samples until state.samples == S
+            for _ in range(-(-S // batch)):
+                state.trace_samples()
+        else:  # a rank's share in calls of B samples
+            for a in range(s0, s1, batch):
+                state.trace_range(a, min(a + batch, s1))
         if red is not None:
             red.submit(img_t if backend == "nccl" else img_t.cpu())
         return state.counters()
@@ -292,6 +311,7 @@ def main():
         img_final = (reduced[0].detach().cpu().numpy().reshape(H, W, 4) if world > 1 else state.get_image())
         sig = image_signature(img_final)
         sig_key = f"{Path(args.scene).stem} {args.sampler} {W}x{H}x{S}spp traversal={traversal}" + \
+            ("".join(f" {o}" for o in sorted(args.opt) if o.split("=")[0] in RESULT_OPTIONS)) + \
             (" bvh=sah" if args.highqualitybvh else "") + \
             (f" rank 0 of {plan_world}" + (f" tiles 1/{groups}" if groups > 1 else "") if partial else "")
         ref_sig = load_signature(SIGNATURES, sig_key)
@@ -312,7 +332,8 @@ def main():
     # hits the slab test's rounding lets one order find and the other cull; exact-t ties re-run in
     # the reference's order)
     ref_order = None
-    if rank == 0 and world == 1 and not partial and args.traversal != "reference" and not args.no_reference_order:
+    if rank == 0 and world == 1 and not partial and args.traversal != "reference" and not args.no_reference_order \
+            and args.batch <= 0:
         img_near = state.get_image()
         rp = abi.make_params(Params(scene=args.scene, samples=args.spp, sampler=2 if args.sampler == "naive" else 1,
                                     width=args.width, height=args.height, device=dev, batch=args.spp,
@@ -435,6 +456,7 @@ def main():
                        "split": {"tile_groups": groups, "sample_ranges": world // groups,
                                  "rank0_share": {"tiles": share or "all", "samples": [s0, s1]}},
                        "sampler": args.sampler, "width": W, "height": H, "spp": S, "bounces": 8,
+                       "batch": batch, "calls_per_step": -(-(s1 - s0) // batch),
                        "traversal": traversal, "traversal_requested": args.traversal,
                        "bvh": "sah" if args.highqualitybvh else "middle",
                        "parallelism": f"{groups} tile groups x {world // groups} sample ranges + RCCL reduce"},

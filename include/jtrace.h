@@ -43,7 +43,8 @@
 extern "C" {
 #endif
 
-#define JT_ABI_VERSION 4  /* 2: jt_params.traversal; 3: jt_set_option; 4: sample streams, jt_get_streams */
+#define JT_ABI_VERSION 5  /* 2: jt_params.traversal; 3: jt_set_option; 4: sample streams, jt_get_streams;
+                            5: deferred jt_trace_range (same signatures) */
 
 typedef enum jt_status {
     JT_OK = 0,
@@ -277,7 +278,8 @@ int jt_device_count(int32_t* out);
  *                            of upper_bound: the same distribution, so results equal the default
  *                            statistically, NOT bitwise (a variant, off by default)
  *   "features" "all"         run the general kernel instead of the scene's specialisation
- *   "lds_scene" "<bytes>"    budget of the small-scene LDS blob (0: scene arrays stay in HBM)
+ *   "lds_scene" "<bytes>"    budget of the small-scene LDS blob (0: scene arrays stay in HBM;
+ *                            the stream count, hence the bits, never depend on the mode)
  *   "lds_stack" "32"         a 32-entry LDS stack ring instead of 16
  *   "light_inline" "0"       sample_lights_pdf's light queries through the traversal loop
  *   "wait_lanes", "light_lanes"  the shading gate; the light-hit step gate
@@ -330,9 +332,18 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
  * jt_get_device_buffers returns device 0's share. */
 int jt_create_multi(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,
                     const jt_params* params, const int32_t* devices, int32_t ndevices, jt_ctx** out);
-/* trace_samples (src/trace.jl:215-274): samples [n, min(n+batch, samples)), n += batch. */
+/* trace_samples (src/trace.jl:215-274): samples [n, min(n+batch, samples)), n += batch
+ * (jt_trace_range of that range: it may return before the samples are traced). */
 int jt_trace_samples(jt_ctx* ctx);
 /* Accumulate global samples [sample_begin, sample_end) into the running mean, in order.
+ * Deferred: the range is queued behind the ranges queued before it and all are traced together
+ * (one launch per 64 samples or so) once 64 samples are queued, the context's params.samples are
+ * reached, or the context is read: jt_get_image / jt_get_aovs / jt_get_counters /
+ * jt_get_device_buffers / jt_synchronize trace the queued samples first and report their errors
+ * (a failed launch then marks the context failed, as an immediate one would). A context whose
+ * device buffers were handed out (jt_get_device_buffers) traces every range at once. Merging
+ * changes only the launch count (jt_counters.launches), never the bits (below). jt_get_samples
+ * counts queued samples; jt_reset drops them.
  * Sample streams (fixed per context, jt_get_streams: k, a power of two): local sample
  * t = s - first_sample (first_sample: the first sample this context ever traced, 0 for a single
  * device) belongs to stream j = t mod k and is the c-th sample of that stream, c = t div k; every
@@ -343,18 +354,25 @@ int jt_trace_samples(jt_ctx* ctx);
  * starting from mean_0 * w_0); hits = sum_j hits_j. k = 1 is the reference's single running mean.
  * The result does not depend on how a render is split into calls. */
 int jt_trace_range(jt_ctx* ctx, int32_t sample_begin, int32_t sample_end);
-/* The context's sample streams per pixel k (jt_trace_range). Chosen by jt_create: 1 when
+/* The context's sample streams per pixel k (jt_trace_range). Chosen by jt_create from the
+ * pixels it traces and the batch only (never the scene or its LDS/HBM mode): 1 when
  * params->batch is 1 (the reference's default); otherwise the smallest power of two k >= 16
- * (>= 32 for a scene too large for LDS mode and a batch of at least 64; jt_describe reports the
- * mode) with (pixels the context traces) * k >= 2^22, reduced to
- * at most 64, the batch, and (pixels) * k <= 2^27 (at least 1); or the "streams" option. */
+ * (>= 32 for a batch of at least 64) with (pixels the context traces) * k >= 2^22, reduced to
+ * at most 64, the batch, and (pixels) * k <= 2^27 (at least 1) — halved further while the
+ * stream means (48 B per pixel and stream) cannot be allocated; or the "streams" option.
+ * k = 1 contexts trace a range of m > 1 samples as chunks of one-sample streams folded into the
+ * single running mean in sample order: the bits of one launch per sample. */
 int jt_get_streams(const jt_ctx* ctx, int32_t* streams);
 int jt_get_samples(const jt_ctx* ctx, int32_t* samples);
 int jt_get_size(const jt_ctx* ctx, int32_t* width, int32_t* height);
 int jt_get_image(jt_ctx* ctx, float* rgba);                          /* W*H*4 */
 int jt_get_aovs(jt_ctx* ctx, float* albedo, float* normal, int64_t* hits); /* W*H*3, W*H*3, W*H */
 int jt_get_counters(jt_ctx* ctx, jt_counters* out);
-int jt_reset(jt_ctx* ctx);                                           /* zero accumulators, samples = 0 */
+/* zero accumulators (at once if their device pointers were handed out, else before they are
+ * next read or overwritten), samples = 0, queued samples dropped */
+int jt_reset(jt_ctx* ctx);
+/* the accumulators' device pointers, current: queued samples are traced first, and from now on
+ * every jt_trace_range traces at once and jt_reset zeroes at once */
 int jt_get_device_buffers(jt_ctx* ctx, jt_device_buffers* out);
 /* Counter level of subsequent launches: 1 (default) counts every jt_counters field; 0 counts
  * paths, rays and light_queries only (the timed production kernel; the other fields are

@@ -21,6 +21,8 @@
 #ifndef JT_AUTO_WIDE_MIN_STACK
 #define JT_AUTO_WIDE_MIN_STACK 32  // JT_TRAVERSAL_AUTO: wide records for HBM-mode scenes deeper than this
 #endif
+// jt_trace_range defers its range until this many samples are queued (jt_ctx::pend0)
+#define JT_DEFER_SAMPLES 64
 #ifndef JT_MAX_STREAMS
 #define JT_MAX_STREAMS 64  // sample streams per pixel (a power of two, jt_ctx::streams)
 #endif

@@ -1399,12 +1399,14 @@ struct DAccum {
                                    // [8..31]: the stamps build's per-phase clocks (JT_STAMPS)
     unsigned* work;                // unit counters of the launch, one per XCD band at work[16 b]
                                    // (zeroed before each launch)
-    // sample-stream means (P.lk > 0): stream j of pixel p at [j * npix + p]; image RGBA, albedo
-    // xyz + the stream's hit count (int bits in w), normal xyz
+    // sample-stream means (P.lk > 0): stream j of a pixel at [j * nslot + slot], slot = the pixel's
+    // place in the launch's tiles (item_slot: launch tile u * 64 + pixel of the tile), so a tile
+    // share stores only its own pixels; image RGBA, albedo xyz + the stream's hit count (int bits
+    // in w), normal xyz
     float4* part_img;
     float4* part_alb;
     float4* part_nrm;
-    int npix;
+    int nslot;  // launch tiles x 64 (the allocation's slots per stream)
 };
 
 // Work units: (8x8 pixel tile t, stream slot q), fetched by whole waves from atomic counters, so
@@ -1462,6 +1464,12 @@ constexpr unsigned ITEM_NONE = 0xffffffffu;
 __device__ __forceinline__ int item_pixel(unsigned item, const DParams& P, int tiles_x) {
     const int t = (int)(item >> 6), l = (int)(item & 63u);
     return ((t / tiles_x) * 8 + (l >> 3)) * P.width + (t % tiles_x) * 8 + (l & 7);
+}
+// an item's slot among the launch's tiles (DAccum::part_*): tiles offset, offset + stride, ... are
+// launch tiles 0, 1, ...
+__host__ __device__ __forceinline__ int item_slot(unsigned item, const DParams& P) {
+    const int t = (int)(item >> 6);
+    return (P.tile_stride == 1 ? t - P.tile_offset : (t - P.tile_offset) / P.tile_stride) * 64 + (int)(item & 63u);
 }
 // running-mean weight of global sample s within its stream
 __device__ __forceinline__ float stream_weight(const DParams& P, int s) {
@@ -1586,7 +1594,8 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                             nr = A.normal[pixel];
                             h = (int)A.hits[pixel];
                         } else {
-                            const size_t o = (size_t)((s - P.first) & (kstr - 1)) * (size_t)A.npix + (size_t)pixel;
+                            const size_t o = (size_t)((s - P.first) & (kstr - 1)) * (size_t)A.nslot +
+                                             (size_t)item_slot(item, P);
                             im = A.part_img[o];
                             al = A.part_alb[o];
                             nr = A.part_nrm[o];
@@ -1793,7 +1802,8 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                         A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
                         A.hits[pixel] = (long long)acc_i[10 * BLOCK];
                     } else {
-                        const size_t o = (size_t)((sample - P.first) & (kstr - 1)) * (size_t)A.npix + (size_t)pixel;
+                        const size_t o = (size_t)((sample - P.first) & (kstr - 1)) * (size_t)A.nslot +
+                                         (size_t)item_slot(item, P);
                         A.part_img[o] = im;
                         A.part_alb[o] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], __int_as_float(acc_i[10 * BLOCK]));
                         A.part_nrm[o] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);

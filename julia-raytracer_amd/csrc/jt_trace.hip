@@ -86,7 +86,18 @@ struct jt_ctx {
     int kmask = FT_ALL;  // feature mask of the kernel specialisation the scene runs
     bool wide = false;   // JT_TRAVERSAL_WIDE: the wide-record kernels (configurations 8-15)
     int traversal = 0;   // jt_params.traversal as resolved (JT_TRAVERSAL_AUTO: near or wide)
-    int first = -1, next = 0;  // running-mean origin and next expected sample
+    int first = -1, next = 0;  // running-mean origin and next expected sample (deferred ones included)
+    // Deferred samples [pend0, pend1): jt_trace_range / jt_trace_samples queue their range and
+    // trace it, merged with the ranges queued before it, once JT_DEFER_SAMPLES are queued or when
+    // anything reads the context (flush). A render split into calls gives the bits of one call
+    // (jt_trace_range's contract), so merging changes only the launch count: the reference's
+    // default --batch 1 (one call per sample) runs as launches of many samples each.
+    int pend0 = 0, pend1 = 0;
+    // one-stream contexts (lk == 0): a flushed range of m > 1 samples runs as chunks of up to
+    // `chunk` samples, each traced as one-sample streams into the stream-mean buffers (allocated at
+    // the first such flush) and folded into the running mean by chain_kernel in sample order
+    int chunk = 0;
+    bool exported = false;  // jt_get_device_buffers handed out the accumulators' device pointers
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     bool failed = false;       // a launch failed: the running means are unusable
     bool stale = true;         // the accumulators are not yet zeroed or overwritten since jt_reset
@@ -111,7 +122,7 @@ struct jt_ctx {
 
 namespace jtk {
 // the combine of every pixel's stream means (DCombine, jt_kernels.h), one thread per pixel of
-// the launch's tiles; stream j's records of neighbouring pixels are contiguous (coalesced)
+// the launch's tiles (slot g); stream j's records of neighbouring pixels are contiguous (coalesced)
 __global__ __launch_bounds__(256) void combine_kernel(DParams P, DAccum A, DCombine Cw) {
     const int tiles_x = (P.width + 7) / 8, tiles = launch_tiles(P);
     const int g = (int)(blockIdx.x * 256 + threadIdx.x);
@@ -119,8 +130,8 @@ __global__ __launch_bounds__(256) void combine_kernel(DParams P, DAccum A, DComb
     const int t = (g >> 6) * P.tile_stride + P.tile_offset, l = g & 63;
     const int i = (t % tiles_x) * 8 + (l & 7), j = (t / tiles_x) * 8 + (l >> 3);
     if (i >= P.width || j >= P.height) return;
-    const size_t pixel = (size_t)j * P.width + i, np = (size_t)A.npix;
-    float4 im = A.part_img[pixel], al = A.part_alb[pixel], nr = A.part_nrm[pixel];
+    const size_t pixel = (size_t)j * P.width + i, ns = (size_t)A.nslot;
+    float4 im = A.part_img[g], al = A.part_alb[g], nr = A.part_nrm[g];
     const float w0 = Cw.w[0];
     long long h = __float_as_int(al.w);
     im = make_float4(im.x * w0, im.y * w0, im.z * w0, im.w * w0);
@@ -130,10 +141,47 @@ __global__ __launch_bounds__(256) void combine_kernel(DParams P, DAccum A, DComb
 #pragma unroll 4
     for (int s = 1; s < Cw.ns; s++) {
         const float w = Cw.w[s];
-        const float4 a = A.part_img[s * np + pixel], b = A.part_alb[s * np + pixel], c = A.part_nrm[s * np + pixel];
+        const float4 a = A.part_img[s * ns + g], b = A.part_alb[s * ns + g], c = A.part_nrm[s * ns + g];
         im = make_float4(im.x + a.x * w, im.y + a.y * w, im.z + a.z * w, im.w + a.w * w);
         al = make_float4(al.x + b.x * w, al.y + b.y * w, al.z + b.z * w, 0.0f);
         nr = make_float4(nr.x + c.x * w, nr.y + c.y * w, nr.z + c.z * w, 0.0f);
+        h += __float_as_int(b.w);
+    }
+    A.image[pixel] = im;
+    A.albedo[pixel] = al;
+    A.normal[pixel] = nr;
+    A.hits[pixel] = h;
+}
+
+// A chunk of a one-stream context (k = 1, the reference's single running mean): the chunk's
+// samples x .. x+m-1 were traced as m one-sample streams (each record = that sample's value:
+// 0 * 0 + value * 1), and are folded into the running mean here one by one, in sample order, with
+// the epilogue's own operations (mean * (1 - w) + value * w, w = 1 / (n0 + j + 1): src/trace.jl:
+// 631-648, src/math.jl:89-93) — bit for bit the image of tracing the samples one launch each.
+// n0: the context's samples before the chunk (0: the mean starts from zero, as after jt_reset).
+__global__ __launch_bounds__(256) void chain_kernel(DParams P, DAccum A, int n0, int m) {
+    const int tiles_x = (P.width + 7) / 8, tiles = launch_tiles(P);
+    const int g = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (g >= tiles * 64) return;
+    const int t = (g >> 6) * P.tile_stride + P.tile_offset, l = g & 63;
+    const int i = (t % tiles_x) * 8 + (l & 7), j = (t / tiles_x) * 8 + (l >> 3);
+    if (i >= P.width || j >= P.height) return;
+    const size_t pixel = (size_t)j * P.width + i, ns = (size_t)A.nslot;
+    float4 im = make_float4(0, 0, 0, 0), al = im, nr = im;
+    long long h = 0;
+    if (n0 > 0) {
+        im = A.image[pixel];
+        al = A.albedo[pixel];
+        nr = A.normal[pixel];
+        h = A.hits[pixel];
+    }
+#pragma unroll 4
+    for (int s = 0; s < m; s++) {
+        const float w = 1.0f / (float)(n0 + s + 1), omw = 1 - w;
+        const float4 a = A.part_img[s * ns + g], b = A.part_alb[s * ns + g], c = A.part_nrm[s * ns + g];
+        im = make_float4(im.x * omw + a.x * w, im.y * omw + a.y * w, im.z * omw + a.z * w, im.w * omw + a.w * w);
+        al = make_float4(al.x * omw + b.x * w, al.y * omw + b.y * w, al.z * omw + b.z * w, 0.0f);
+        nr = make_float4(nr.x * omw + c.x * w, nr.y * omw + c.y * w, nr.z * omw + c.z * w, 0.0f);
         h += __float_as_int(b.w);
     }
     A.image[pixel] = im;
@@ -430,20 +478,22 @@ int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_wo
 // the launch schedule: a unit counter per XCD band
 constexpr size_t SCHED_BYTES = (size_t)NBANDS * BAND_STRIDE * 4;
 
-// Sample streams per pixel (DESIGN.md §2 "Sample streams"), fixed at jt_create: 1 for the
-// reference's default one-sample batches (its single running mean); otherwise at least 16 (a
-// stream item is then at most a sixteenth of a batch's samples: the launch ends on short items)
-// and enough for 2^22 (pixel, stream) items (a context tracing few pixels — a tile share, a small
-// image — still fills the GPU), at most 64, the batch, and 2^27 items of stream means (6.4 GB).
+// Sample streams per pixel (DESIGN.md §2 "Sample streams"), fixed at jt_create from the pixels
+// the context traces and the batch only (never from the scene's memory mode, so every option
+// that picks LDS or HBM mode keeps the image bits): 1 for the reference's default one-sample
+// batches (its single running mean); otherwise at least 16 — 32 from a batch of 64 (two samples
+// per stream) — and enough for 2^22 (pixel, stream) items (a context tracing few pixels — a tile
+// share, a small image — still fills the GPU), at most 64, the batch, and 2^27 items of stream
+// means (6.4 GB).
 // Measured (gpurun_out/r05i, r05j): bathroom1 1024 spp 8 -> 16 streams +0.8 %, features2 512 spp
 // +2 %, ecosys 64 spp 2 -> 16 +2.6 %, its 1/8 share (512 spp) +3.7 %; a 1/8 tile share of the
 // headline 32 streams 9265, 64 streams 9794 Mrays/s. A context whose scene runs from HBM starts
 // from 32 streams when the batch gives each at least two samples (gpurun_out/r05sk, r05sk2:
-// features2 +0.6 %, bathroom1 +0.5 %); an LDS-mode one (cornellbox) keeps 16: 32 gained it 1.0 %
-// but doubled its stream-mean stores (1.9 GB per launch). The option "streams" overrides.
-int stream_log2(long long pixels, int batch, bool hbm_scene) {
+// features2 +0.6 %, bathroom1 +0.5 %; cornellbox +1.0 %, round 5, when 32 streams were the
+// HBM-mode rule only). The option "streams" overrides.
+int stream_log2(long long pixels, int batch) {
     if (batch <= 1) return 0;
-    long long want = hbm_scene && batch >= 2 * JT_STREAMS_WIDE ? JT_STREAMS_WIDE : JT_STREAMS_MIN;
+    long long want = batch >= 2 * JT_STREAMS_WIDE ? JT_STREAMS_WIDE : JT_STREAMS_MIN;
     while (pixels * want < JT_STREAM_ITEMS) want *= 2;
     int lk = 0;
     while (lk < 6 && (2LL << lk) <= want && (2 << lk) <= batch && (2 << lk) <= JT_MAX_STREAMS &&
@@ -1176,8 +1226,10 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
         }
     }
     // sample streams: from the pixels this context traces (a tile share traces 1/stride of them)
-    c->lk = stream_log2(((long long)W * H + P.tile_stride - 1) / P.tile_stride, std::max(1, params->batch), S.blob_n16 == 0);
+    c->lk = stream_log2(((long long)W * H + P.tile_stride - 1) / P.tile_stride, std::max(1, params->batch));
+    bool forced_streams = false;
     if (const char* ks = opt("streams")) {
+        forced_streams = true;
         const int k = std::atoi(ks);
         if (k < 1 || k > JT_MAX_STREAMS || (k & (k - 1)) != 0)
             return bail(jt::fail(JT_ERR_INVALID, "option streams: a power of two in [1, " + std::to_string(JT_MAX_STREAMS) + "]"));
@@ -1225,19 +1277,31 @@ int jt_create(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* l
     void* sched = nullptr;
     if ((e = hipMalloc(&sched, SCHED_BYTES)) != hipSuccess) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc schedule"));
     c->allocations.push_back(sched);
-    // the sample streams' means (k > 1): image, albedo + hits, normal per (stream, pixel)
+    // the sample streams' means (k > 1): image, albedo + hits, normal per (stream, slot of the
+    // launch's tiles: a tile share holds only its own pixels). Too little memory for k streams
+    // halves k (the image bits then follow the smaller k, jt_get_streams) unless the option
+    // "streams" asked for this k.
     void* part[3] = {nullptr, nullptr, nullptr};
-    if (c->lk > 0) {
+    const size_t nslot = (size_t)launch_tiles(P) * 64;
+    while (c->lk > 0) {
+        bool ok = true;
+        for (int k = 0; k < 3 && ok; k++) ok = hipMalloc(&part[k], nslot * 16 << c->lk) == hipSuccess;
+        if (ok) break;
+        (void)hipGetLastError();
         for (int k = 0; k < 3; k++) {
-            if ((e = hipMalloc(&part[k], np * 16 << c->lk)) != hipSuccess)
-                return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc stream means"));
-            c->allocations.push_back(part[k]);
+            if (part[k]) (void)hipFree(part[k]);
+            part[k] = nullptr;
         }
+        if (forced_streams) return bail(jt::fail(JT_ERR_NOMEM, "hipMalloc stream means"));
+        c->lk--;
     }
+    for (int k = 0; k < 3; k++)
+        if (part[k]) c->allocations.push_back(part[k]);
+    P.lk = c->lk;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, params->device) == hipSuccess && cus > 0) c->cus = cus;
     c->A = DAccum{(float4*)img, (float4*)alb, (float4*)nrmb, (long long*)hits, (unsigned long long*)cnt, (unsigned*)sched,
-                  (float4*)part[0], (float4*)part[1], (float4*)part[2], (int)np};
+                  (float4*)part[0], (float4*)part[1], (float4*)part[2], (int)nslot};
     st = jt_reset(c);
     if (st != JT_OK) return bail(st);
     *out = c;
@@ -1343,6 +1407,7 @@ int jt_reset(jt_ctx* c) {
             if (st != JT_OK) return st;
         }
         std::fill(c->nsub.begin(), c->nsub.end(), 0LL);
+        c->pend0 = c->pend1 = 0;  // deferred samples are dropped with the state
         c->first = -1;
         c->next = 0;
         c->failed = false;
@@ -1356,9 +1421,12 @@ int jt_reset(jt_ctx* c) {
     // make_trace_state's zeroed buffers (src/trace.jl:189-213). A context that traces every tile
     // overwrites every pixel in its first launch without reading it (a stream's first sample
     // starts from zero), so they are zeroed only if read before that launch (zero_if_stale); a
-    // tile share keeps the other tiles' pixels at zero for the reduce, so it zeroes them now.
+    // tile share keeps the other tiles' pixels at zero for the reduce, and a context whose device
+    // buffers were handed out is read in place, so those zero them now.
     c->stale = true;
-    if (c->P.tile_stride != 1) {
+    c->pend0 = c->pend1 = 0;  // deferred samples are dropped with the state
+    // a caller holding the device pointers (jt_get_device_buffers) sees the zeros at once
+    if (c->P.tile_stride != 1 || c->exported) {
         const int st = zero_if_stale(c);
         if (st != JT_OK) return st;
     }
@@ -1374,35 +1442,92 @@ int jt_reset(jt_ctx* c) {
 }  // extern "C"
 
 namespace {
-// enqueue one launch over global samples [s0, s1) of a context whose local samples start at
-// `first` (stream t & (k-1) of local sample t = s - first, DParams::lk), then — with k > 1 — the
-// combine of every pixel's stream means into the image and AOV buffers
-int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
-    c->P.first = first;
+// the chunk size of a one-stream context: as many one-sample streams as the stream-mean buffers
+// hold, at most 64 (JT_MAX_STREAMS) and 2^27 (stream, slot) records (6.4 GB); allocated at the
+// first multi-sample range, halved on NOMEM. 0 after jt_create (none yet), 1: none possible.
+int ensure_chunk(jt_ctx* c) {
+    if (c->chunk) return JT_OK;
+    const long long nslot = (long long)launch_tiles(c->P) * 64;
+    int m = JT_MAX_STREAMS;
+    while (m > 1 && nslot * m > JT_STREAM_ITEMS_MAX) m >>= 1;
     (void)hipSetDevice(c->device);
+    for (; m > 1; m >>= 1) {
+        void* part[3] = {nullptr, nullptr, nullptr};
+        bool ok = true;
+        for (int k = 0; k < 3 && ok; k++) ok = hipMalloc(&part[k], (size_t)nslot * 16 * (size_t)m) == hipSuccess;
+        if (ok) {
+            for (int k = 0; k < 3; k++) c->allocations.push_back(part[k]);
+            c->A.part_img = (float4*)part[0];
+            c->A.part_alb = (float4*)part[1];
+            c->A.part_nrm = (float4*)part[2];
+            c->A.nslot = (int)nslot;
+            break;
+        }
+        (void)hipGetLastError();
+        for (int k = 0; k < 3; k++)
+            if (part[k]) (void)hipFree(part[k]);
+    }
+    c->chunk = m;
+    return JT_OK;
+}
+
+// enqueue the trace launch of global samples [s0, s1) for local samples starting at `first`
+// (stream t & (k-1) of local sample t = s - first, DParams::lk), then — with k > 1 — the combine
+// of every pixel's stream means into the image and AOV buffers
+int launch_range(jt_ctx* c, const DParams& P, int32_t s0, int32_t s1) {
     hipError_t e = hipMemsetAsync(c->A.work, 0, SCHED_BYTES, c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
-    if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if (c->sampler == JT_SAMPLER_NAIVE)
-        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<2, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<2, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, c->A, c->stream, c->cus);
     else
-        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<1, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, c->P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, c->A, c->stream, c->cus)
+                     : launch_s<1, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, c->A, c->stream, c->cus);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
-    if (c->lk > 0) {
-        // weights n_j / n of the streams after this launch: n local samples, stream j holds
-        // those t < n with t mod k == j (include/jtrace.h jt_get_streams restates the rule)
-        const long long n = (long long)s1 - first, k = 1LL << c->lk;
-        DCombine cw{};
-        cw.ns = (int)std::min(n, k);
-        for (int j = 0; j < cw.ns; j++) cw.w[j] = (float)((double)((n - 1 - j) / k + 1) / (double)n);
-        const int tiles = launch_tiles(c->P);
-        const int nblk = (int)(((long long)tiles * 64 + 255) / 256);
-        if (nblk > 0) hipLaunchKernelGGL(combine_kernel, dim3(nblk), dim3(256), 0, c->stream, c->P, c->A, cw);
-        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "combine kernel launch");
+    return JT_OK;
+}
+
+// enqueue the launches of global samples [s0, s1) of a context whose local samples start at
+// `first`. k > 1 streams: one trace launch + the combine. k = 1 (the reference's single running
+// mean): one launch for one sample; a longer range in chunks (jt_ctx::chunk) of one-sample streams,
+// each folded into the running mean by chain_kernel — the bits of one launch per sample, with
+// m times the items per launch
+int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
+    (void)hipSetDevice(c->device);
+    hipError_t e;
+    if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    const int tiles = launch_tiles(c->P);
+    const int nblk = (int)(((long long)tiles * 64 + 255) / 256);
+    int launches = 0;
+    if (c->lk == 0 && s1 - s0 > 1 && ensure_chunk(c) == JT_OK && c->chunk > 1) {
+        for (int32_t x = s0; x < s1; x += c->chunk) {
+            const int32_t y = std::min(s1, x + c->chunk);
+            DParams P = c->P;  // the chunk's samples as one-sample streams x .. y-1
+            P.first = x;
+            P.lk = 0;
+            while ((1 << P.lk) < y - x) P.lk++;
+            if (const int st = launch_range(c, P, x, y)) return st;
+            if (nblk > 0) hipLaunchKernelGGL(chain_kernel, dim3(nblk), dim3(256), 0, c->stream, c->P, c->A, x - first, y - x);
+            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "chain kernel launch");
+            launches++;
+        }
+    } else {
+        c->P.first = first;
+        if (const int st = launch_range(c, c->P, s0, s1)) return st;
+        launches = 1;
+        if (c->lk > 0) {
+            // weights n_j / n of the streams after this launch: n local samples, stream j holds
+            // those t < n with t mod k == j (include/jtrace.h jt_get_streams restates the rule)
+            const long long n = (long long)s1 - first, k = 1LL << c->lk;
+            DCombine cw{};
+            cw.ns = (int)std::min(n, k);
+            for (int j = 0; j < cw.ns; j++) cw.w[j] = (float)((double)((n - 1 - j) / k + 1) / (double)n);
+            if (nblk > 0) hipLaunchKernelGGL(combine_kernel, dim3(nblk), dim3(256), 0, c->stream, c->P, c->A, cw);
+            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "combine kernel launch");
+        }
     }
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    c->launches += launches - 1;  // trace_finish counts one
     c->stale = false;  // every pixel of the launch's tiles was written (tile shares were zeroed at reset)
     return JT_OK;
 }
@@ -1514,6 +1639,20 @@ int multi_reduce(jt_ctx* c, int which, float* out4, int64_t* hits) {
     else e = hipMemcpy(hits, c->red_hits, np * 8, hipMemcpyDeviceToHost);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipMemcpy reduce");
 }
+
+// trace the deferred samples [pend0, pend1) (jt_ctx) and wait for them; every call that reads
+// the context's results or device buffers runs this first
+int flush(jt_ctx* c) {
+    if (c->pend1 <= c->pend0) return JT_OK;
+    const int32_t s0 = c->pend0, s1 = c->pend1;
+    c->pend0 = c->pend1 = 0;
+    if (!c->sub.empty()) return multi_trace_range(c, s0, s1);
+    int st = trace_launch(c, s0, s1, c->first);
+    float ms = 0;
+    if (st == JT_OK) st = trace_finish(c, &ms);
+    if (st != JT_OK) c->failed = true;
+    return st;
+}
 }  // namespace
 
 extern "C" {
@@ -1526,15 +1665,14 @@ int jt_trace_range(jt_ctx* c, int32_t s0, int32_t s1) {
     if (c->first >= 0 && s0 != c->next)
         return jt::fail(JT_ERR_STATE, "samples must be accumulated in order (expected " + std::to_string(c->next) + ")");
     if (c->first < 0) c->first = s0;
-    if (!c->sub.empty()) return multi_trace_range(c, s0, s1);
-    int st = trace_launch(c, s0, s1, c->first);
-    float ms = 0;
-    if (st == JT_OK) st = trace_finish(c, &ms);
-    if (st != JT_OK) {
-        c->failed = true;
-        return st;
-    }
+    // queue the range behind the deferred ones (jt_ctx::pend0); trace them all once enough are
+    // queued, the render is complete (params.samples: the end of Jtrace.main's loop), or a caller
+    // reads the accumulators in place (jt_get_device_buffers: it sees every range at once)
+    if (c->pend1 <= c->pend0) c->pend0 = s0;
+    c->pend1 = s1;
     c->next = s1;
+    const bool in_place = c->exported || (!c->sub.empty() && c->sub[0]->exported);
+    if (in_place || c->pend1 - c->pend0 >= JT_DEFER_SAMPLES || c->next >= c->total_samples) return flush(c);
     return JT_OK;
 }
 
@@ -1567,6 +1705,7 @@ int jt_get_size(const jt_ctx* c, int32_t* w, int32_t* h) {
 
 int jt_get_image(jt_ctx* c, float* rgba) {
     if (!c || !rgba) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    if (const int st = flush(c)) return st;
     if (c->failed) return jt::fail(JT_ERR_STATE, "the running means are corrupt (a launch failed); jt_reset the context");
     if (!c->sub.empty()) {
         for (jt_ctx* s : c->sub)
@@ -1581,6 +1720,7 @@ int jt_get_image(jt_ctx* c, float* rgba) {
 
 int jt_get_aovs(jt_ctx* c, float* albedo, float* normal, int64_t* hits) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    if (const int st = flush(c)) return st;
     if (c->failed) return jt::fail(JT_ERR_STATE, "the running means are corrupt (a launch failed); jt_reset the context");
     for (jt_ctx* s : c->sub)
         if (const int st = zero_if_stale(s)) return st;
@@ -1628,6 +1768,7 @@ int jt_get_aovs(jt_ctx* c, float* albedo, float* normal, int64_t* hits) {
 
 int jt_get_counters(jt_ctx* c, jt_counters* out) {
     if (!c || !out) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    if (const int st = flush(c)) return st;
     if (!c->sub.empty()) {  // summed over the devices; kernel_ms: per launch the slowest device
         jt_counters sum{};
         for (jt_ctx* s : c->sub) {
@@ -1665,8 +1806,10 @@ int jt_get_counters(jt_ctx* c, jt_counters* out) {
 
 int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
     if (!c || !out) return jt::fail(JT_ERR_INVALID, "NULL argument");
+    if (const int st = flush(c)) return st;
     if (!c->sub.empty()) return jt_get_device_buffers(c->sub[0], out);  // device 0's share
     if (const int st = zero_if_stale(c)) return st;
+    c->exported = true;  // jt_reset now zeroes the buffers at once (the caller may read them)
     out->image = c->A.image;
     out->albedo = c->A.albedo;
     out->normal = c->A.normal;
@@ -1726,6 +1869,7 @@ int jt_set_counters(jt_ctx* c, int32_t level) {
 
 int jt_synchronize(jt_ctx* c) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
+    if (const int st = flush(c)) return st;
     for (jt_ctx* s : c->sub) {
         const int st = jt_synchronize(s);
         if (st != JT_OK) return st;

@@ -341,6 +341,9 @@ typedef struct ctx_s {
     wtree_t* wblas;    /* and every BLAS's */
     fr3 camera_frame;
     float camera_aspect; /* cam.aspect, or W/H when --width/--height are given (see setup_ctx) */
+    /* the build's env_alias option (or_set_env_alias): per light, its alias table or NULL */
+    float** alias_keep;
+    int32_t** alias_other;
     int width, height;
 } ctx_t;
 
@@ -1504,6 +1507,73 @@ static float sample_delta_pdf(const material_point* m, v3 n, v3 o, v3 i) {
 static inline v3 eval_emission(const material_point* m, v3 normal, v3 outgoing) {
     return dot3(normal, outgoing) >= 0 ? m->emission : V3(0, 0, 0);
 }
+/* ---- environment-light alias tables: the build's `env_alias` option (include/jtrace.h,
+ * SURVEY §8(f) rank 3), restated here so that option has a seeded checker. The reference draws an
+ * environment texel with sample_discrete = upper_bound over the texel CDF (src/sampling.jl:33-56,
+ * src/trace.jl:989); the option draws from the same pmf, p_i = cdf[i] - cdf[i-1]
+ * (sample_discrete_pdf, src/sampling.jl:39-40), in O(1) with Vose's alias method:
+ *   column    c = clamp(trunc(rel * n), 0, n - 1)             (float product, then truncation)
+ *   texel idx = (ruv.x < keep[c] ? c : other[c]) + 1           (1-based, as sample_discrete's)
+ * The random numbers are the ones the light branch already draws (Appendix A: rl, rel, ruv.x,
+ * ruv.y; an environment sample of the reference never reads ruv), so the RNG stream is unchanged.
+ * Which CDFs get a table: environment lights whose CDF has >= 1024 entries, is non-decreasing and
+ * ends finite and positive (the others keep upper_bound). Table: probabilities scaled to mean 1 in
+ * double, columns paired by two LIFO worklists filled in index order (small: < 1, large: >= 1);
+ * leftovers of either list keep their own column with probability 1. */
+static int g_env_alias = 0;
+void or_set_env_alias(int32_t on) { g_env_alias = on != 0; }
+
+static int alias_wanted(const jt_light* l) {
+    if (l->environment < 0 || l->ncdf < 1024) return 0;
+    for (int32_t i = 1; i < l->ncdf; i++)
+        if (!(l->cdf[i] >= l->cdf[i - 1])) return 0;
+    const float last = l->cdf[l->ncdf - 1];
+    return last > 0 && isfinite(last);
+}
+static int build_alias(const float* cdf, int32_t n, float* keep, int32_t* other) {
+    double* q = (double*)malloc(sizeof(double) * (size_t)n);
+    int32_t* small = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+    int32_t* large = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+    if (!q || !small || !large) { free(q); free(small); free(large); return JT_ERR_NOMEM; }
+    double total = 0;
+    for (int32_t i = 0; i < n; i++) {
+        double p = (double)cdf[i] - (i > 0 ? (double)cdf[i - 1] : 0.0);
+        q[i] = p > 0 ? p : 0.0;
+        total += q[i];
+    }
+    int32_t ns = 0, nl = 0;
+    for (int32_t i = 0; i < n; i++) {
+        q[i] = total > 0 ? q[i] * (double)n / total : 1.0;
+        if (q[i] < 1.0) small[ns++] = i;
+        else large[nl++] = i;
+    }
+    while (ns > 0 && nl > 0) {
+        const int32_t a = small[--ns], b = large[nl - 1];
+        keep[a] = (float)q[a];
+        other[a] = b;
+        q[b] -= 1.0 - q[a];
+        if (q[b] < 1.0) {
+            nl--;
+            small[ns++] = b;
+        }
+    }
+    for (int32_t k = 0; k < nl; k++) { keep[large[k]] = 1.0f; other[large[k]] = large[k]; }
+    for (int32_t k = 0; k < ns; k++) { keep[small[k]] = 1.0f; other[small[k]] = small[k]; }
+    free(q);
+    free(small);
+    free(large);
+    return JT_OK;
+}
+/* the table of one CDF (tests/test_oracle_kat.py): 0 or a negative jt_status */
+int or_alias_table(const float* cdf, int32_t n, float* keep, int32_t* other) {
+    if (!cdf || n <= 0 || !keep || !other) return JT_ERR_INVALID;
+    return build_alias(cdf, n, keep, other);
+}
+static long sample_alias(const float* keep, const int32_t* other, long n, float rel, float coin) {
+    long col = jl_clampi((long)(rel * (float)n), 0, n - 1);
+    return (coin < keep[col] ? col : (long)other[col]) + 1;
+}
+
 /* sample_lights (src/trace.jl:968-1008) */
 static v3 sample_lights(const ctx_t* c, v3 position, float rl, float rel, v2 ruv) {
     long light_id = sample_uniform(c->lights->nlights, rl);
@@ -1518,7 +1588,10 @@ static v3 sample_lights(const ctx_t* c, v3 position, float rl, float rel, v2 ruv
     } else if (light->environment >= 0) {
         const jt_environment* env = &c->scene->environments[light->environment];
         const jt_texture* tex = &c->scene->textures[env->emission_tex];
-        long idx = sample_discrete(light->cdf, light->ncdf, rel); /* 1-based, used as-is (:990-993) */
+        const long li = light - c->lights->lights;
+        long idx = c->alias_keep && c->alias_keep[li]  /* 1-based, used as-is (:990-993) */
+                       ? sample_alias(c->alias_keep[li], c->alias_other[li], light->ncdf, rel, ruv.x)
+                       : sample_discrete(light->cdf, light->ncdf, rel);
         float u = ((float)(idx % tex->width) + 0.5f) / (float)tex->width;
         float v = (float)((((double)idx / (double)tex->width) + 0.5) / (double)tex->height);
         v3 dir = V3(jl_cos(u * 2 * pif) * jl_sin(v * pif), jl_cos(v * pif), jl_sin(u * 2 * pif) * jl_sin(v * pif));
@@ -1937,6 +2010,20 @@ static int setup_ctx(ctx_t* c, const jt_scene* scene, const jt_scene_bvh* bvh, c
         c->env_frame[k] = frame_from(scene->environments[k].frame);
         c->env_inverse[k] = inverse_frame(&c->env_frame[k], 0);
     }
+    if (g_env_alias) {
+        c->alias_keep = (float**)calloc((size_t)lights->nlights + 1, sizeof(float*));
+        c->alias_other = (int32_t**)calloc((size_t)lights->nlights + 1, sizeof(int32_t*));
+        if (!c->alias_keep || !c->alias_other) return JT_ERR_NOMEM;
+        for (int k = 0; k < lights->nlights; k++) {
+            const jt_light* l = &lights->lights[k];
+            if (!alias_wanted(l)) continue;
+            c->alias_keep[k] = (float*)malloc(sizeof(float) * (size_t)l->ncdf);
+            c->alias_other[k] = (int32_t*)malloc(sizeof(int32_t) * (size_t)l->ncdf);
+            if (!c->alias_keep[k] || !c->alias_other[k]) return JT_ERR_NOMEM;
+            int st = build_alias(l->cdf, l->ncdf, c->alias_keep[k], c->alias_other[k]);
+            if (st != JT_OK) return st;
+        }
+    }
     if (params->traversal == JT_TRAVERSAL_WIDE) {
         c->wblas = (wtree_t*)calloc((size_t)scene->nshapes + 1, sizeof(wtree_t));
         if (!c->wblas) return JT_ERR_NOMEM;
@@ -1957,6 +2044,13 @@ static void free_ctx(ctx_t* c) {
     if (c->wblas)
         for (int s = 0; s < c->scene->nshapes; s++) free(c->wblas[s].r);
     free(c->wblas);
+    if (c->alias_keep)
+        for (int k = 0; k < c->lights->nlights; k++) {
+            free(c->alias_keep[k]);
+            free(c->alias_other[k]);
+        }
+    free(c->alias_keep);
+    free(c->alias_other);
 }
 
 static int trace_rows_impl(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_lights* lights,

@@ -51,6 +51,13 @@ int or_trace_rows(const jt_scene* scene, const jt_scene_bvh* bvh, const jt_light
                   float* part_alb, float* part_nrm, int64_t* part_hits, int32_t nthreads,
                   or_counters* counters);
 
+/* The build's env_alias option (include/jtrace.h jt_set_option "env_alias"): environment lights
+ * draw their texel through Vose alias tables instead of upper_bound (jt_oracle.c, "alias
+ * tables"). Applies to contexts set up after the call (or_trace*). */
+void or_set_env_alias(int32_t on);
+/* that alias table of one CDF: keep[i] (probability of keeping column i), other[i] (0-based) */
+int or_alias_table(const float* cdf, int32_t n, float* keep, int32_t* other);
+
 /* Single-function known-answer entry points (tests/test_oracle_kat.py). */
 int or_intersect_triangle(const float* o, const float* d, float tmin, float tmax,
                           const float* p1, const float* p2, const float* p3, float* out_uvt);

@@ -48,6 +48,9 @@ def _load(abi):
     lib.or_inverse_frame.restype = None
     lib.or_srgb_to_rgb.argtypes = [C.POINTER(C.c_uint8), C.c_int32, f32p]
     lib.or_srgb_to_rgb.restype = None
+    lib.or_set_env_alias.argtypes = [C.c_int32]
+    lib.or_set_env_alias.restype = None
+    lib.or_alias_table.argtypes = [f32p, C.c_int32, f32p, C.POINTER(C.c_int32)]
     lib.or_wide_check.argtypes = [C.POINTER(abi.jt_bvh_tree), C.POINTER(abi.jt_bvh_tree), C.c_int32,
                                   C.POINTER(C.c_int64)]
     return lib
@@ -81,6 +84,17 @@ class Oracle:
             raise RuntimeError(f"oracle lights failed: {st}")
         return _Owned(out, self.lib.or_free_lights)
 
+    def alias_table(self, cdf):
+        """The env_alias option's Vose table of one light CDF: (keep (n,) float32, other (n,) int32)."""
+        cdf = np.ascontiguousarray(cdf, np.float32)
+        keep = np.empty(len(cdf), np.float32)
+        other = np.empty(len(cdf), np.int32)
+        st = self.lib.or_alias_table(cdf.ctypes.data_as(C.POINTER(C.c_float)), len(cdf),
+                                     keep.ctypes.data_as(C.POINTER(C.c_float)), other.ctypes.data_as(C.POINTER(C.c_int32)))
+        if st != 0:
+            raise RuntimeError(f"oracle alias table failed: {st}")
+        return keep, other
+
     def wide_check(self, bvh):
         """The wide records of every tree of `bvh` (JT_TRAVERSAL_WIDE): dict of records,
         non-conservative children (must be 0), leaves, mean dequantised/exact box volume ratio."""
@@ -92,13 +106,16 @@ class Oracle:
         return {"records": out[0], "violations": out[1], "leaves": out[2], "volume_ratio": out[3] / 1000.0}
 
     def trace(self, scene_abi, bvh, lights, params, width, height, s0, s1, first=0, rows=None,
-              nthreads=None, state=None, streams=1, parts=None):
+              nthreads=None, state=None, streams=1, parts=None, env_alias=False):
         """Returns (image (H,W,4), albedo (H,W,3), normal (H,W,3), hits (H,W), counters).
 
         streams: the sample streams per pixel k (a power of two, the library's jt_get_streams;
         include/jtrace.h jt_trace_range states the contract). For k > 1 the streams' running
         means are kept in `parts` (a dict of arrays, created when None and filled in place), which
-        a caller passes again to continue the same render with a later range."""
+        a caller passes again to continue the same render with a later range.
+
+        env_alias: restate the library's env_alias option (environment texels drawn through
+        alias tables, oracle/jt_oracle.c) for this call."""
         if params.traversal not in (0, 1, 2):
             raise ValueError(f"the oracle restates an explicit BVH order (0 reference, 1 near, 2 wide), got "
                              f"{params.traversal}: resolve auto (3) to the order the library ran first")
@@ -131,13 +148,24 @@ class Oracle:
             pp = (None, None, None, None)
         r0, r1 = rows if rows is not None else (0, height)
         cnt = Counters()
-        st = self.lib.or_trace_rows(scene_abi.ref, C.byref(bvh.struct), C.byref(lights.struct), C.byref(params),
-                                    width, height, r0, r1, first, s0, s1, image.ctypes.data_as(f32p),
-                                    albedo.ctypes.data_as(f32p), normal.ctypes.data_as(f32p),
-                                    hits.ctypes.data_as(i64p), lk, *pp, nthreads, C.byref(cnt))
+        self.lib.or_set_env_alias(int(bool(env_alias)))
+        try:
+            st = self._trace_rows(scene_abi, bvh, lights, params, width, height, r0, r1, first, s0, s1, image, albedo,
+                                  normal, hits, lk, pp, nthreads, cnt)
+        finally:
+            self.lib.or_set_env_alias(0)
         if st != 0:
             raise RuntimeError(f"oracle trace failed: {st}")
         return image, albedo, normal, hits, cnt.as_dict()
+
+    def _trace_rows(self, scene_abi, bvh, lights, params, width, height, r0, r1, first, s0, s1, image, albedo,
+                    normal, hits, lk, pp, nthreads, cnt):
+        f32p = C.POINTER(C.c_float)
+        i64p = C.POINTER(C.c_int64)
+        return self.lib.or_trace_rows(scene_abi.ref, C.byref(bvh.struct), C.byref(lights.struct), C.byref(params),
+                                    width, height, r0, r1, first, s0, s1, image.ctypes.data_as(f32p),
+                                    albedo.ctypes.data_as(f32p), normal.ctypes.data_as(f32p),
+                                    hits.ctypes.data_as(i64p), lk, *pp, nthreads, C.byref(cnt))
 
 
     def order_diff(self, scene_abi, bvh, lights, params, alt_traversal, width, height, s0, s1, nthreads=None):

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_version(lib):
-    assert lib.jt_abi_version() == 4  # 2: jt_params.traversal, 3: jt_set_option, 4: sample streams
+    assert lib.jt_abi_version() == 5  # 2: jt_params.traversal, 3: jt_set_option, 4: sample streams, 5: deferred ranges
     assert b"gfx950" in lib.jt_version()
 
 

@@ -1,15 +1,17 @@
 """Environment-light alias tables (option env_alias=1; SURVEY §8(f) rank 3, src/trace.jl:968-1008 and
 src/sampling.jl:33-56): an O(1) Vose alias draw replaces upper_bound over the environment CDF.
 It samples the same pmf but maps random numbers to texels differently, so it cannot be
-bit-exact with the reference's upper_bound: it is a non-default statistical variant. Checked
-here (1) against the reference's own renders through the same block-mean pins as the default
-path (tests/test_gpu_scenes.py::test_statistical_pin_reference_render), and (2) against the
-default (bit-exact, oracle-checked) path at equal sample counts: channel means and ray counts
-within noise, images not identical (the variant really ran)."""
+bit-exact with the reference's upper_bound: a non-default variant. Checked here (1) against the
+oracle's seeded restatement of the same tables and draw (oracle/jt_oracle.c "alias tables") at
+the parity bar of tests/test_gpu_parity.py, on every scene with an environment light the
+configs and feature scenes hold; (2) against the reference's own renders through the same
+block-mean pins as the default path (tests/test_gpu_scenes.py::test_statistical_pin_reference_render);
+(3) against the default path at equal sample counts: channel means and ray counts within noise,
+images not identical (the variant really ran)."""
 import numpy as np
 import pytest
 
-from conftest import make_params
+from conftest import compare_images, make_params
 import test_gpu_scenes as tgs
 from test_gpu_scenes import scene_abi
 
@@ -29,6 +31,28 @@ def _render(abi, lib, sa, p, spp, alias, options):
     out = (st.get_image(), st.counters(), st.describe())
     st.close()
     return out
+
+
+@pytest.mark.parametrize("sampler", [1, 2])
+@pytest.mark.parametrize("name", ["features1", "features2", "ecosys"])
+def test_alias_matches_the_oracle(gpu, abi, lib, oracle, options, name, sampler):
+    """HIP with env_alias=1 vs the oracle's restatement of the alias tables and draw: image at the
+    §8(c) bar with >= 99.9 % of pixels bit-identical, hits exact, counters within the rare flipped
+    path; the naive sampler never samples lights, so there the option must change nothing."""
+    sa = scene_abi(name)
+    p = make_params(abi, resolution=120, samples=6, sampler=sampler)
+    options("env_alias", "1")
+    g = tgs.render_gpu(lib, sa, p, 0, 6)
+    options("env_alias", None)
+    o = tgs.oracle_with(oracle, sa, p, g[0].shape[1], g[0].shape[0], 0, 6, env_alias=True)
+    tgs.check_parity(g, o, f"{name}/{sampler} env_alias")
+    stats = compare_images(g[0], o[0])
+    assert stats["bitwise_frac"] >= 0.999, stats
+    d = tgs.oracle_with(oracle, sa, p, g[0].shape[1], g[0].shape[0], 0, 6, env_alias=False)
+    if sampler == 2:
+        assert np.array_equal(o[0], d[0])
+    else:
+        assert not np.array_equal(o[0], d[0])  # the alias draw really ran on both sides
 
 
 @pytest.mark.parametrize("name", ["features1", "features2"])

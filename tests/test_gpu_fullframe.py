@@ -67,6 +67,7 @@ def test_full_frame_band_parity(gpu, abi, lib, oracle, name, order, band):
     stats = compare_images(g[0], o[0])
     print(f"{name} traversal={order} rows [{r0}, {r1}) {desc.split()[0]}: {stats}")
     assert stats["frac_pix_rel_le_1e-3"] >= 0.999, stats
+    assert stats["bitwise_frac"] >= 0.999, stats  # a silent 1-ulp regression shows here
     assert stats["image_mean_rel"] <= 1e-4, stats
     assert np.array_equal(g[3], o[3])
     for a, b in ((g[1], o[1]), (g[2], o[2])):
