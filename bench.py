@@ -429,7 +429,8 @@ def main():
             roof.update(traffic=int(traffic), hbm_achieved_gbs=round(traffic / avg_launch_s / 1e9, 1),
                         hbm_frac=round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5))
             roof["binding"] = {k: d[k] for k in ("valu_issue_frac", "lane_util", "fp32_lane_frac", "td_busy_frac",
-                                                 "td_unstalled_frac", "td_tc_stall_frac_of_busy", "l2_hit_rate",
+                                                 "td_unstalled_frac", "td_tc_stall_frac_of_busy", "l2_hit_rate", "l1_hit_rate",
+                                                 "l1_accesses_per_vmem_rd", "l1_misses_per_vmem_rd",
                                                  "vmem_mix_frac", "vmem_mix_frac_resident", "clock_ghz") if k in d}
             roof["binding"]["write_bytes_per_launch"] = int(d["write_bytes"])
             roof["binding"]["profiled_launch_ms"] = round(rec["duration_ns"] / 1e6, 3)

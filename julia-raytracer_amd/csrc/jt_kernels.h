@@ -1466,10 +1466,14 @@ __device__ __forceinline__ int item_pixel(unsigned item, const DParams& P, int t
     return ((t / tiles_x) * 8 + (l >> 3)) * P.width + (t % tiles_x) * 8 + (l & 7);
 }
 // an item's slot among the launch's tiles (DAccum::part_*): tiles offset, offset + stride, ... are
-// launch tiles 0, 1, ...
+// launch tiles 0, 1, ...; (t - offset) / stride is exact, and t < 2^20 keeps the float quotient
+// within 2^-3 of it. Against the integer division: cornellbox +0.5 %, its 1/8 share +0.9 % (two
+// runs each, profiles/r06_ab/slot_float_vs_div_r06d.txt; the division's code raised the kernels'
+// spills from 1-2 to 4-6 VGPRs)
 __host__ __device__ __forceinline__ int item_slot(unsigned item, const DParams& P) {
     const int t = (int)(item >> 6);
-    return (P.tile_stride == 1 ? t - P.tile_offset : (t - P.tile_offset) / P.tile_stride) * 64 + (int)(item & 63u);
+    const int u = (int)((float)(t - P.tile_offset) * (1.0f / (float)P.tile_stride) + 0.5f);
+    return u * 64 + (int)(item & 63u);
 }
 // running-mean weight of global sample s within its stream
 __device__ __forceinline__ float stream_weight(const DParams& P, int s) {

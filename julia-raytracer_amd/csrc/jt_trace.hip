@@ -352,8 +352,64 @@ float exp_scale(int e) {  // 2^(e - 127), e = a normal float's biased exponent
     std::memcpy(&f, &b, 4);
     return f;
 }
-// The binary leaves of a tree in the order the wide records list them: records breadth-first (as
-// build_wide appends them), within a record its leaf children in slot order. The device lays out
+// The wide records of a binary tree: one per internal node N (or the root leaf), holding N's
+// grandchildren in slots [LL, LR, RL, RR] (a leaf child takes the pair's first slot alone).
+void wide_slots(const jt_bvh_tree& t, int n, int slot[4]) {
+    slot[0] = slot[1] = slot[2] = slot[3] = -1;
+    const jt_bvh_node& N = t.nodes[n];
+    if (!N.internal) {
+        slot[0] = n;
+        return;
+    }
+    const int L = N.start, R = N.start + 1;
+    if (t.nodes[L].internal) slot[0] = t.nodes[L].start, slot[1] = t.nodes[L].start + 1;
+    else slot[0] = L;
+    if (t.nodes[R].internal) slot[2] = t.nodes[R].start, slot[3] = t.nodes[R].start + 1;
+    else slot[2] = R;
+}
+// Storage order of the wide records (the binary node each record stands for). JT_WIDE_ORDER 0:
+// breadth-first. 1: sibling groups depth-first — a record's internal children are stored
+// together, then each child's subtree in slot order, so a subtree is one contiguous run of
+// records (a ray descending it stays in a few pages and L2 sets). Storage only: the traversal
+// visits the same records in the same order. Measured against breadth-first (two runs each,
+// profiles/r06_ab/wide_order_dfs_vs_bfs_r06d.txt): bathroom1 1920x1080x64 +0.1 %, ecosys
+// 3840x2160x8 +0.2 %: within noise, so breadth-first stays the default.
+#ifndef JT_WIDE_ORDER
+#define JT_WIDE_ORDER 0
+#endif
+std::vector<int> wide_record_order(const jt_bvh_tree& t) {
+    std::vector<int> seq;
+    if (t.nnodes <= 0) return seq;
+    seq.push_back(0);
+    if (JT_WIDE_ORDER == 0) {
+        for (size_t h = 0; h < seq.size(); h++) {
+            if (!t.nodes[seq[h]].internal) continue;
+            int slot[4];
+            wide_slots(t, seq[h], slot);
+            for (int c = 0; c < 4; c++)
+                if (slot[c] >= 0 && t.nodes[slot[c]].internal) seq.push_back(slot[c]);
+        }
+        return seq;
+    }
+    // depth-first over sibling groups, iterative: a stack of the records whose children are still
+    // to be appended (their subtrees then follow in slot order)
+    std::vector<int> st{0};
+    while (!st.empty()) {
+        const int n = st.back();
+        st.pop_back();
+        if (!t.nodes[n].internal) continue;
+        int slot[4];
+        wide_slots(t, n, slot);
+        int kids[4], nk = 0;
+        for (int c = 0; c < 4; c++)
+            if (slot[c] >= 0 && t.nodes[slot[c]].internal) kids[nk++] = slot[c];
+        for (int c = 0; c < nk; c++) seq.push_back(kids[c]);
+        for (int c = nk - 1; c >= 0; c--) st.push_back(kids[c]);
+    }
+    return seq;
+}
+// The binary leaves of a tree in the order the wide records list them: records in storage order
+// (wide_record_order), within a record its leaf children in slot order. The device lays out
 // primitive records and numbers instances in this order, so a record's leaf children are
 // consecutive runs (a record could address them from one start) and every binary leaf is
 // still one run (the binary traversal addresses a leaf by its start). Measured against node-index
@@ -367,30 +423,19 @@ std::vector<int> wide_leaf_order(const jt_bvh_tree& t) {
         order.push_back(0);
         return order;
     }
-    std::vector<int> q{0};
-    for (size_t h = 0; h < q.size(); h++) {
-        const jt_bvh_node& N = t.nodes[q[h]];
-        int slot[4] = {-1, -1, -1, -1};
-        const int L = N.start, R = N.start + 1;
-        if (t.nodes[L].internal) slot[0] = t.nodes[L].start, slot[1] = t.nodes[L].start + 1;
-        else slot[0] = L;
-        if (t.nodes[R].internal) slot[2] = t.nodes[R].start, slot[3] = t.nodes[R].start + 1;
-        else slot[2] = R;
-        for (int c = 0; c < 4; c++) {
-            if (slot[c] < 0) continue;
-            if (t.nodes[slot[c]].internal) q.push_back(slot[c]);
-            else order.push_back(slot[c]);
-        }
+    for (int n : wide_record_order(t)) {
+        int slot[4];
+        wide_slots(t, n, slot);
+        for (int c = 0; c < 4; c++)
+            if (slot[c] >= 0 && !t.nodes[slot[c]].internal) order.push_back(slot[c]);
     }
     return order;
 }
 
-// The wide records of one binary tree, appended to `out` breadth-first (global indices =
-// positions in `out`). A record stands for an internal node N (or the root leaf) and holds N's
-// grandchildren in slots [LL, LR, RL, RR] (a leaf child takes the pair's first slot alone), their
-// boxes quantised relative to N's box per axis at the smallest scale 2^(e-127) >= extent / 255
-// (and the next larger ones until every child fits). leaf_word(k): the child word of binary leaf
-// k. Returns the root record's index, or -1 with the error set.
+// The wide records of one binary tree, appended to `out` in wide_record_order (global indices =
+// positions in `out`), their boxes quantised relative to N's box per axis at the smallest scale
+// 2^(e-127) >= extent / 255 (and the next larger ones until every child fits). leaf_word(k): the
+// child word of binary leaf k. Returns the root record's index, or -1 with the error set.
 int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_word, std::vector<DWide>& out) {
     if (t.nnodes <= 0 || (!t.nodes[0].internal && t.nodes[0].num <= 0)) {
         // an empty tree (make_bvh of no boxes is one leaf without primitives, src/bvh.jl:138-183):
@@ -400,40 +445,26 @@ int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_wo
         out.push_back(w);
         return (int)out.size() - 1;
     }
-    std::vector<int> q{0}, rec{(int)out.size()};
-    out.emplace_back();
-    for (size_t h = 0; h < q.size(); h++) {
-        const jt_bvh_node& N = t.nodes[q[h]];
-        int slot[4] = {-1, -1, -1, -1}, a1 = 0, a2 = 0;
-        if (!N.internal) {
-            slot[0] = q[h];
-        } else {
-            const int L = N.start, R = N.start + 1;
-            if (t.nodes[L].internal) {
-                slot[0] = t.nodes[L].start;
-                slot[1] = t.nodes[L].start + 1;
-                a1 = t.nodes[L].axis;
-            } else {
-                slot[0] = L;
-            }
-            if (t.nodes[R].internal) {
-                slot[2] = t.nodes[R].start;
-                slot[3] = t.nodes[R].start + 1;
-                a2 = t.nodes[R].axis;
-            } else {
-                slot[2] = R;
-            }
+    const std::vector<int> seq = wide_record_order(t);
+    const size_t base = out.size();
+    if (base + seq.size() > (size_t)IDX_MASK) return jt::fail(JT_ERR_UNSUPPORTED, "scene exceeds 2^24 wide records"), -1;
+    std::vector<int> rec_of(t.nnodes, -1);  // binary internal node -> its record
+    for (size_t h = 0; h < seq.size(); h++) rec_of[seq[h]] = (int)(base + h);
+    out.resize(base + seq.size());
+    for (size_t h = 0; h < seq.size(); h++) {
+        const jt_bvh_node& N = t.nodes[seq[h]];
+        int slot[4], a1 = 0, a2 = 0;
+        wide_slots(t, seq[h], slot);
+        if (N.internal) {
+            if (t.nodes[N.start].internal) a1 = t.nodes[N.start].axis;
+            if (t.nodes[N.start + 1].internal) a2 = t.nodes[N.start + 1].axis;
         }
         unsigned word[4] = {W_EMPTY, W_EMPTY, W_EMPTY, W_EMPTY};
         for (int c = 0; c < 4; c++) {
             if (slot[c] < 0) continue;
             const jt_bvh_node& C = t.nodes[slot[c]];
             if (C.internal) {
-                if (out.size() >= (size_t)IDX_MASK) return jt::fail(JT_ERR_UNSUPPORTED, "scene exceeds 2^24 wide records"), -1;
-                word[c] = (unsigned)out.size();
-                q.push_back(slot[c]);
-                rec.push_back((int)out.size());
-                out.emplace_back();
+                word[c] = (unsigned)rec_of[slot[c]];
             } else {
                 if (C.num < 1 || C.num > 4) return jt::fail(JT_ERR_UNSUPPORTED, "wide traversal: a BVH leaf outside 1..4 primitives"), -1;
                 word[c] = leaf_word(slot[c]);
@@ -464,7 +495,7 @@ int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_wo
             e3[ax] = (unsigned)e;
         }
         auto bytes = [](const unsigned* v) { return v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24; };
-        DWide& W = out[rec[h]];
+        DWide& W = out[base + h];
         const unsigned meta = e3[0] | e3[1] << 8 | e3[2] << 16 |
                               ((unsigned)(N.internal ? N.axis : 0) | (unsigned)a1 << 2 | (unsigned)a2 << 4) << 24;
         W.r0 = make_float4(N.bmin[0], N.bmin[1], N.bmin[2], as_f(meta));
@@ -472,7 +503,7 @@ int build_wide(const jt_bvh_tree& t, const std::function<unsigned(int)>& leaf_wo
         W.r2 = make_uint4(bytes(lo[2]), bytes(hi[2]), 0u, 0u);
         W.r3 = make_uint4(word[0], word[1], word[2], word[3]);
     }
-    return rec[0];
+    return (int)base;
 }
 
 // the launch schedule: a unit counter per XCD band

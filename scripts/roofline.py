@@ -171,6 +171,12 @@ def derive(rec):
             # L1 (TCP) cache accesses per vector-memory read wave-instruction (a divergent gather
             # touches one line per distinct address)
             out["l1_accesses_per_vmem_rd"] = pmc["TCP_TOTAL_CACHE_ACCESSES_sum"] / pmc["SQ_INSTS_VMEM_RD"]
+        if pmc.get("TCP_TCC_READ_REQ_sum") is not None and pmc.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
+            # L1 (TCP) locality: read requests the L1 sends on to L2 (its misses) per access and per
+            # vector-memory read wave-instruction (the distinct lines a gather misses)
+            out["l1_hit_rate"] = 1.0 - pmc["TCP_TCC_READ_REQ_sum"] / pmc["TCP_TOTAL_CACHE_ACCESSES_sum"]
+            if pmc.get("SQ_INSTS_VMEM_RD"):
+                out["l1_misses_per_vmem_rd"] = pmc["TCP_TCC_READ_REQ_sum"] / pmc["SQ_INSTS_VMEM_RD"]
         if pmc.get("TCP_PENDING_STALL_CYCLES_sum"):
             out["tcp_pending_stall_frac"] = pmc["TCP_PENDING_STALL_CYCLES_sum"] / CUS / gui
         if pmc.get("SQ_WAVE_CYCLES"):

@@ -98,3 +98,31 @@ def test_environment_only_scene(gpu, abi, lib, oracle, order):
     assert f"traversal={order}" in g[5]
     assert g[4]["rays"] > 0 and g[4]["shades"] == 0
     assert float(g[0][..., 3].min()) == 1.0  # the environment is visible everywhere
+
+
+@pytest.mark.parametrize("order", ["near", "wide", "reference"])
+@pytest.mark.parametrize("sampler", [1, 2])
+def test_coplanar_ties_with_opacity(gpu, abi, lib, oracle, cornell, order, sampler):
+    """Exact-t ties combined with opacity < 1: every cornellbox instance gets a
+    coplanar twin (the same shape and frame) with a differently coloured material of opacity 0.6,
+    and every shape repeats its own triangles, so almost every hit is a tie — between two
+    instances (TLAS leaves) and between two triangles of one BLAS leaf — whose winner the
+    reference's child order decides (src/bvh.jl:331-341, src/geometry.jl:226), and the opacity
+    draw of the winner's material (src/trace.jl:336-345) then lets the path skip through and
+    continue from a moved origin. Every traversal order against the oracle's restatement of it
+    (the near-first orders re-run a tied query in the reference's order)."""
+    from jtrace.scene import InstanceData, MaterialData
+    sc = copy.deepcopy(cornell)
+    rng = np.random.default_rng(11)
+    for s in sc.shapes:
+        s.triangles = np.concatenate([s.triangles, s.triangles[::-1]]).astype(np.int32)
+    base_m = len(sc.materials)
+    for m in list(sc.materials):
+        sc.materials.append(MaterialData(type=m.type, emission=m.emission.copy(),
+                                         color=rng.uniform(0.1, 0.9, 3).astype(np.float32), opacity=np.float32(0.6)))
+    twins = [InstanceData(frame=i.frame.copy(), shape=i.shape, material=base_m + i.material, name=i.name + "_twin")
+             for i in sc.instances]
+    sc.instances = [x for pair in zip(sc.instances, twins) for x in pair]
+    g, o = _parity(abi, lib, oracle, sc, f"ties+opacity/{order}/{sampler}", sampler=sampler, traversal=order)
+    assert f"traversal={order}" in g[5] and ",255," in g[5]  # FT_OPAC: the general kernel
+    assert g[3].sum() > 0 and g[4]["light_queries"] > 0 if sampler == 1 else g[3].sum() > 0
