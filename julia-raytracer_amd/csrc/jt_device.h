@@ -12,7 +12,7 @@
 #include <stdint.h>
 
 // automatic stream count (jt_trace.hip stream_log2): at least JT_STREAMS_MIN streams —
-// JT_STREAMS_WIDE for an HBM-mode scene and a batch of at least two samples per such stream — and JT_STREAM_ITEMS
+// JT_STREAMS_WIDE for a batch of at least two samples per such stream — and JT_STREAM_ITEMS
 // (pixel, stream) items, at most JT_STREAM_ITEMS_MAX items
 #define JT_STREAMS_MIN 16
 #define JT_STREAMS_WIDE 32

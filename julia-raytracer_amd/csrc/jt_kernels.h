@@ -1433,8 +1433,10 @@ __host__ __device__ __forceinline__ int launch_tiles(const DParams& P) {
 // of each other — no item waits for another — so a launch has W·H·min(k, samples) concurrent
 // items however few pixels it covers, and the launch ends by combining each pixel's stream means
 // in stream order (combine_kernel, weights n_j / n). k = 1 is the reference's own single running
-// mean (the image buffer is stream 0). Results depend on k (fixed per context, jt_get_streams)
-// and not on how a render is split into calls or launches.
+// mean (the image buffer is stream 0): one sample per launch reads and writes it here; a longer
+// range runs as chunks of one-sample streams folded in sample order (chain_kernel, jt_trace.hip).
+// Results depend on k (fixed per context, jt_get_streams) and not on how a render is split into
+// calls or launches.
 //
 // Per-lane work items: the work units are (8x8 tile, stream), fetched by whole waves, but a lane
 // is not tied to its wave's unit: a lane that has finished its item takes the next pixel of its

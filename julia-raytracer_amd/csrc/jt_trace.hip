@@ -97,6 +97,12 @@ struct jt_ctx {
     // `chunk` samples, each traced as one-sample streams into the stream-mean buffers (allocated at
     // the first such flush) and folded into the running mean by chain_kernel in sample order
     int chunk = 0;
+    // two sets of chunk buffers: chunk i traces into set i & 1 on `stream` while chain_kernel folds
+    // chunk i - 1 on `stream2` (the chains stay in sample order on stream2; a trace reuses a set
+    // only after the chain that read it, chain_done)
+    float4* cpart[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+    hipStream_t stream2 = nullptr;
+    hipEvent_t trace_done[2] = {nullptr, nullptr}, chain_done[2] = {nullptr, nullptr};
     bool exported = false;  // jt_get_device_buffers handed out the accumulators' device pointers
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     bool failed = false;       // a launch failed: the running means are unusable
@@ -159,6 +165,8 @@ __global__ __launch_bounds__(256) void combine_kernel(DParams P, DAccum A, DComb
 // the epilogue's own operations (mean * (1 - w) + value * w, w = 1 / (n0 + j + 1): src/trace.jl:
 // 631-648, src/math.jl:89-93) — bit for bit the image of tracing the samples one launch each.
 // n0: the context's samples before the chunk (0: the mean starts from zero, as after jt_reset).
+// At most 32 VGPRs: the trace kernel of the next chunk (5 waves/SIMD of 96 VGPRs in LDS mode)
+// leaves 32 per SIMD free, so chain waves run on the same CUs beside it (stream2).
 __global__ __launch_bounds__(256) void chain_kernel(DParams P, DAccum A, int n0, int m) {
     const int tiles_x = (P.width + 7) / 8, tiles = launch_tiles(P);
     const int g = (int)(blockIdx.x * 256 + threadIdx.x);
@@ -166,28 +174,35 @@ __global__ __launch_bounds__(256) void chain_kernel(DParams P, DAccum A, int n0,
     const int t = (g >> 6) * P.tile_stride + P.tile_offset, l = g & 63;
     const int i = (t % tiles_x) * 8 + (l & 7), j = (t / tiles_x) * 8 + (l >> 3);
     if (i >= P.width || j >= P.height) return;
-    const size_t pixel = (size_t)j * P.width + i, ns = (size_t)A.nslot;
-    float4 im = make_float4(0, 0, 0, 0), al = im, nr = im;
-    long long h = 0;
+    const unsigned pixel = (unsigned)j * (unsigned)P.width + (unsigned)i;  // jt_create: < 2^26 pixels
+    float ix = 0, iy = 0, iz = 0, iw = 0, ax = 0, ay = 0, az = 0, nx = 0, ny = 0, nz = 0;
+    int h = 0;  // the chunk's hits (< 2^31 samples)
     if (n0 > 0) {
-        im = A.image[pixel];
-        al = A.albedo[pixel];
-        nr = A.normal[pixel];
-        h = A.hits[pixel];
+        const float4 a = A.image[pixel], b = A.albedo[pixel], c = A.normal[pixel];
+        ix = a.x, iy = a.y, iz = a.z, iw = a.w, ax = b.x, ay = b.y, az = b.z, nx = c.x, ny = c.y, nz = c.z;
     }
-#pragma unroll 4
-    for (int s = 0; s < m; s++) {
+    // few live registers (byte offsets below 4 GiB: 2^27 records of 16 B at most per buffer set
+    // and array, jt_ctx::chunk), so the waves fit beside the next chunk's trace kernel
+    const char* pi = reinterpret_cast<const char*>(A.part_img);
+    const char* pa = reinterpret_cast<const char*>(A.part_alb);
+    const char* pn = reinterpret_cast<const char*>(A.part_nrm);
+    const unsigned step = (unsigned)A.nslot * 16u;
+    unsigned off = (unsigned)g * 16u;
+#pragma unroll 1
+    for (int s = 0; s < m; s++, off += step) {
         const float w = 1.0f / (float)(n0 + s + 1), omw = 1 - w;
-        const float4 a = A.part_img[s * ns + g], b = A.part_alb[s * ns + g], c = A.part_nrm[s * ns + g];
-        im = make_float4(im.x * omw + a.x * w, im.y * omw + a.y * w, im.z * omw + a.z * w, im.w * omw + a.w * w);
-        al = make_float4(al.x * omw + b.x * w, al.y * omw + b.y * w, al.z * omw + b.z * w, 0.0f);
-        nr = make_float4(nr.x * omw + c.x * w, nr.y * omw + c.y * w, nr.z * omw + c.z * w, 0.0f);
+        const float4 a = *reinterpret_cast<const float4*>(pi + off);
+        ix = ix * omw + a.x * w, iy = iy * omw + a.y * w, iz = iz * omw + a.z * w, iw = iw * omw + a.w * w;
+        const float4 b = *reinterpret_cast<const float4*>(pa + off);
+        ax = ax * omw + b.x * w, ay = ay * omw + b.y * w, az = az * omw + b.z * w;
         h += __float_as_int(b.w);
+        const float4 c = *reinterpret_cast<const float4*>(pn + off);
+        nx = nx * omw + c.x * w, ny = ny * omw + c.y * w, nz = nz * omw + c.z * w;
     }
-    A.image[pixel] = im;
-    A.albedo[pixel] = al;
-    A.normal[pixel] = nr;
-    A.hits[pixel] = h;
+    A.image[pixel] = make_float4(ix, iy, iz, iw);
+    A.albedo[pixel] = make_float4(ax, ay, az, 0.0f);
+    A.normal[pixel] = make_float4(nx, ny, nz, 0.0f);
+    A.hits[pixel] = (n0 > 0 ? A.hits[pixel] : 0LL) + h;
 }
 
 }  // namespace jtk
@@ -593,9 +608,15 @@ void jt_destroy(jt_ctx* c) {
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     for (void* p : c->allocations) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (int k = 0; k < 2; k++) {
+        if (c->trace_done[k]) (void)hipEventDestroy(c->trace_done[k]);
+        if (c->chain_done[k]) (void)hipEventDestroy(c->chain_done[k]);
+    }
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1448,6 +1469,8 @@ int jt_reset(jt_ctx* c) {
     }
     (void)hipSetDevice(c->device);
     hipError_t e;
+    // a failed flush may have left chains queued on stream2 (a complete one ends on `stream`)
+    if (c->stream2 && (e = hipStreamSynchronize(c->stream2)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     if ((e = hipMemsetAsync(c->A.counters, 0, 256, c->stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     // make_trace_state's zeroed buffers (src/trace.jl:189-213). A context that traces every tile
     // overwrites every pixel in its first launch without reading it (a stream's first sample
@@ -1473,29 +1496,37 @@ int jt_reset(jt_ctx* c) {
 }  // extern "C"
 
 namespace {
-// the chunk size of a one-stream context: as many one-sample streams as the stream-mean buffers
-// hold, at most 64 (JT_MAX_STREAMS) and 2^27 (stream, slot) records (6.4 GB); allocated at the
-// first multi-sample range, halved on NOMEM. 0 after jt_create (none yet), 1: none possible.
+// the chunk size of a one-stream context: as many one-sample streams as two sets of stream-mean
+// buffers hold, at most 64 (JT_MAX_STREAMS) and 2^27 (stream, slot) records in all (6.4 GB);
+// allocated at the first multi-sample range, halved on NOMEM. 0 after jt_create (none yet), 1:
+// none possible (the range then runs as one launch of long items).
 int ensure_chunk(jt_ctx* c) {
     if (c->chunk) return JT_OK;
     const long long nslot = (long long)launch_tiles(c->P) * 64;
     int m = JT_MAX_STREAMS;
-    while (m > 1 && nslot * m > JT_STREAM_ITEMS_MAX) m >>= 1;
+    while (m > 1 && 2 * nslot * m > JT_STREAM_ITEMS_MAX) m >>= 1;
     (void)hipSetDevice(c->device);
+    if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+        c->stream2 = nullptr;
+        m = 1;
+    }
+    for (int k = 0; k < 2 && m > 1; k++)
+        if (hipEventCreateWithFlags(&c->trace_done[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->chain_done[k], hipEventDisableTiming) != hipSuccess)
+            m = 1;
     for (; m > 1; m >>= 1) {
-        void* part[3] = {nullptr, nullptr, nullptr};
+        void* part[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
         bool ok = true;
-        for (int k = 0; k < 3 && ok; k++) ok = hipMalloc(&part[k], (size_t)nslot * 16 * (size_t)m) == hipSuccess;
+        for (int k = 0; k < 6 && ok; k++) ok = hipMalloc(&part[k], (size_t)nslot * 16 * (size_t)m) == hipSuccess;
         if (ok) {
-            for (int k = 0; k < 3; k++) c->allocations.push_back(part[k]);
-            c->A.part_img = (float4*)part[0];
-            c->A.part_alb = (float4*)part[1];
-            c->A.part_nrm = (float4*)part[2];
-            c->A.nslot = (int)nslot;
+            for (int k = 0; k < 6; k++) {
+                c->allocations.push_back(part[k]);
+                c->cpart[k / 3][k % 3] = (float4*)part[k];
+            }
             break;
         }
         (void)hipGetLastError();
-        for (int k = 0; k < 3; k++)
+        for (int k = 0; k < 6; k++)
             if (part[k]) (void)hipFree(part[k]);
     }
     c->chunk = m;
@@ -1505,15 +1536,15 @@ int ensure_chunk(jt_ctx* c) {
 // enqueue the trace launch of global samples [s0, s1) for local samples starting at `first`
 // (stream t & (k-1) of local sample t = s - first, DParams::lk), then — with k > 1 — the combine
 // of every pixel's stream means into the image and AOV buffers
-int launch_range(jt_ctx* c, const DParams& P, int32_t s0, int32_t s1) {
+int launch_range(jt_ctx* c, const DParams& P, const DAccum& A, int32_t s0, int32_t s1) {
     hipError_t e = hipMemsetAsync(c->A.work, 0, SCHED_BYTES, c->stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync schedule");
     if (c->sampler == JT_SAMPLER_NAIVE)
-        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<2, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<2, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, A, c->stream, c->cus)
+                     : launch_s<2, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, A, c->stream, c->cus);
     else
-        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, c->A, c->stream, c->cus)
-                     : launch_s<1, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, c->A, c->stream, c->cus);
+        e = c->count ? launch_s<1, 1>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, A, c->stream, c->cus)
+                     : launch_s<1, 0>(c->stack, c->ring, c->kmask, c->wide, c->S, P, s0, s1, A, c->stream, c->cus);
     if (e != hipSuccess) return hip_fail(e, "trace kernel launch");
     return JT_OK;
 }
@@ -1531,20 +1562,38 @@ int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
     const int nblk = (int)(((long long)tiles * 64 + 255) / 256);
     int launches = 0;
     if (c->lk == 0 && s1 - s0 > 1 && ensure_chunk(c) == JT_OK && c->chunk > 1) {
-        for (int32_t x = s0; x < s1; x += c->chunk) {
+        // chunk i traces into buffer set i & 1 on `stream`; its chain runs on `stream2` after that
+        // trace and after chain i - 1 (stream order), overlapping trace i + 1; trace i + 2 reuses
+        // the set once chain i has read it. `stream` then waits for the last chain (ev1 covers it).
+        int i = 0;
+        for (int32_t x = s0; x < s1; x += c->chunk, i++) {
             const int32_t y = std::min(s1, x + c->chunk);
+            const int set = i & 1;
             DParams P = c->P;  // the chunk's samples as one-sample streams x .. y-1
             P.first = x;
             P.lk = 0;
             while ((1 << P.lk) < y - x) P.lk++;
-            if (const int st = launch_range(c, P, x, y)) return st;
-            if (nblk > 0) hipLaunchKernelGGL(chain_kernel, dim3(nblk), dim3(256), 0, c->stream, c->P, c->A, x - first, y - x);
+            DAccum A = c->A;
+            A.part_img = c->cpart[set][0];
+            A.part_alb = c->cpart[set][1];
+            A.part_nrm = c->cpart[set][2];
+            A.nslot = tiles * 64;
+            if (i >= 2 && (e = hipStreamWaitEvent(c->stream, c->chain_done[set], 0)) != hipSuccess)
+                return hip_fail(e, "hipStreamWaitEvent");
+            if (const int st = launch_range(c, P, A, x, y)) return st;
+            if ((e = hipEventRecord(c->trace_done[set], c->stream)) != hipSuccess ||
+                (e = hipStreamWaitEvent(c->stream2, c->trace_done[set], 0)) != hipSuccess)
+                return hip_fail(e, "hipEventRecord");
+            if (nblk > 0) hipLaunchKernelGGL(chain_kernel, dim3(nblk), dim3(256), 0, c->stream2, c->P, A, x - first, y - x);
             if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "chain kernel launch");
+            if ((e = hipEventRecord(c->chain_done[set], c->stream2)) != hipSuccess) return hip_fail(e, "hipEventRecord");
             launches++;
         }
+        if ((e = hipStreamWaitEvent(c->stream, c->chain_done[(i - 1) & 1], 0)) != hipSuccess)
+            return hip_fail(e, "hipStreamWaitEvent");
     } else {
         c->P.first = first;
-        if (const int st = launch_range(c, c->P, s0, s1)) return st;
+        if (const int st = launch_range(c, c->P, c->A, s0, s1)) return st;
         launches = 1;
         if (c->lk > 0) {
             // weights n_j / n of the streams after this launch: n local samples, stream j holds

@@ -7,7 +7,7 @@
 #   bench:<w>[:<extra args>]   one bench.py line for workload <w> (table below), with its CPU and
 #                              reference-order legs unless the extra args skip them
 #   quick:<w>[:<extra args>]   a bench.py line without the CPU / reference-order legs (A/B runs)
-#   measure:<w>                the roofline evidence of workload <w> (scripts/gpu_measure.sh)
+#   measure:<w>[:<extra args>] the roofline evidence of workload <w> (scripts/gpu_measure.sh)
 #   sig:<w>                    write workload <w>'s one-GPU image signature (bench --write-signature)
 #   ab:<w>:<lib>,<lib>...      A/B of library builds (build/libjtrace_hip[_<lib>].so, "base" = the
 #                              product build), each twice, interleaved
@@ -86,8 +86,8 @@ for task in "$@"; do
             $S 400 "$O/sig_$name.log" python bench.py --no-cpu-baseline --no-reference-order --write-signature $(wargs "$w") --steps 1 --warmup 0 || exit 1
             cp profiles/image_signatures.json "$O/image_signatures.json" ;;
         measure)
-            wl=$(python bench.py --print-workload $(wargs "$w")) || exit 1
-            bash scripts/gpu_measure.sh "$O/m_$name" "$wl" $(wargs "$w") || exit 1 ;;
+            wl=$(python bench.py --print-workload $(wargs "$w") $extra) || exit 1
+            bash scripts/gpu_measure.sh "$O/m_$name" "$wl" $(wargs "$w") $extra || exit 1 ;;
         ab)
             for rep in 1 2; do
                 for lib in $(echo "$extra" | tr ',' ' '); do
