@@ -1942,6 +1942,7 @@ int jt_describe(const jt_ctx* c, char* buf, int32_t n) {
 int jt_set_counters(jt_ctx* c, int32_t level) {
     if (!c) return jt::fail(JT_ERR_INVALID, "ctx is NULL");
     if (level != 0 && level != 1) return jt::fail(JT_ERR_INVALID, "counter level must be 0 or 1");
+    if (const int st = flush(c)) return st;  // queued samples are traced at the level they were queued at
     for (jt_ctx* s : c->sub) s->count = level;
     c->count = level;
     return JT_OK;
