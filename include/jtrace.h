@@ -372,7 +372,10 @@ int jt_get_counters(jt_ctx* ctx, jt_counters* out);
  * next read or overwritten), samples = 0, queued samples dropped */
 int jt_reset(jt_ctx* ctx);
 /* the accumulators' device pointers, current: queued samples are traced first, and from now on
- * every jt_trace_range traces at once and jt_reset zeroes at once */
+ * every jt_trace_range traces at once and jt_reset zeroes at once. The image is current when
+ * jt_trace_range returns; with k > 1 streams albedo, normal and hits are combined from the
+ * streams' means only when read, so through these pointers they are current after
+ * jt_synchronize (or jt_get_aovs) */
 int jt_get_device_buffers(jt_ctx* ctx, jt_device_buffers* out);
 /* Counter level of subsequent launches: 1 (default) counts every jt_counters field; 0 counts
  * paths, rays and light_queries only (the timed production kernel; the other fields are

@@ -107,6 +107,10 @@ struct jt_ctx {
     int count = 1;             // 1: all traversal counters (diagnostic), 0: paths/rays/light queries only
     bool failed = false;       // a launch failed: the running means are unusable
     bool stale = true;         // the accumulators are not yet zeroed or overwritten since jt_reset
+    // k > 1: the last launch combined the image only; albedo, normal and hits are combined from
+    // the stream means (weights aov_cw) when first read (finish_aovs)
+    bool aov_pending = false;
+    DCombine aov_cw{};
     bool env_alias = false;    // JT_ENV_ALIAS=1: environment lights sample through alias tables
                                // until jt_reset
     size_t lds_scene_bytes = 0;  // > 0: small-scene LDS mode
@@ -128,7 +132,12 @@ struct jt_ctx {
 
 namespace jtk {
 // the combine of every pixel's stream means (DCombine, jt_kernels.h), one thread per pixel of
-// the launch's tiles (slot g); stream j's records of neighbouring pixels are contiguous (coalesced)
+// the launch's tiles (slot g); stream j's records of neighbouring pixels are contiguous (coalesced).
+// Two kernels over the same streams: the image after every launch (16 B per pixel and stream),
+// the AOVs and hits (32 B per pixel and stream) only when they are read (jt_ctx::aov_pending):
+// the stream means stay in place until the next launch appends to them, so the deferred AOV
+// combine reads exactly what an eager one would have
+template <bool AOV>
 __global__ __launch_bounds__(256) void combine_kernel(DParams P, DAccum A, DCombine Cw) {
     const int tiles_x = (P.width + 7) / 8, tiles = launch_tiles(P);
     const int g = (int)(blockIdx.x * 256 + threadIdx.x);
@@ -137,26 +146,35 @@ __global__ __launch_bounds__(256) void combine_kernel(DParams P, DAccum A, DComb
     const int i = (t % tiles_x) * 8 + (l & 7), j = (t / tiles_x) * 8 + (l >> 3);
     if (i >= P.width || j >= P.height) return;
     const size_t pixel = (size_t)j * P.width + i, ns = (size_t)A.nslot;
-    float4 im = A.part_img[g], al = A.part_alb[g], nr = A.part_nrm[g];
     const float w0 = Cw.w[0];
-    long long h = __float_as_int(al.w);
-    im = make_float4(im.x * w0, im.y * w0, im.z * w0, im.w * w0);
-    al = make_float4(al.x * w0, al.y * w0, al.z * w0, 0.0f);
-    nr = make_float4(nr.x * w0, nr.y * w0, nr.z * w0, 0.0f);
-    // unrolled: four streams' loads in flight per thread (the sums stay in stream order)
+    if constexpr (!AOV) {
+        float4 im = A.part_img[g];
+        im = make_float4(im.x * w0, im.y * w0, im.z * w0, im.w * w0);
+        // unrolled: eight streams' loads in flight per thread (the sums stay in stream order)
+#pragma unroll 8
+        for (int s = 1; s < Cw.ns; s++) {
+            const float w = Cw.w[s];
+            const float4 a = A.part_img[s * ns + g];
+            im = make_float4(im.x + a.x * w, im.y + a.y * w, im.z + a.z * w, im.w + a.w * w);
+        }
+        A.image[pixel] = im;
+    } else {
+        float4 al = A.part_alb[g], nr = A.part_nrm[g];
+        long long h = __float_as_int(al.w);
+        al = make_float4(al.x * w0, al.y * w0, al.z * w0, 0.0f);
+        nr = make_float4(nr.x * w0, nr.y * w0, nr.z * w0, 0.0f);
 #pragma unroll 4
-    for (int s = 1; s < Cw.ns; s++) {
-        const float w = Cw.w[s];
-        const float4 a = A.part_img[s * ns + g], b = A.part_alb[s * ns + g], c = A.part_nrm[s * ns + g];
-        im = make_float4(im.x + a.x * w, im.y + a.y * w, im.z + a.z * w, im.w + a.w * w);
-        al = make_float4(al.x + b.x * w, al.y + b.y * w, al.z + b.z * w, 0.0f);
-        nr = make_float4(nr.x + c.x * w, nr.y + c.y * w, nr.z + c.z * w, 0.0f);
-        h += __float_as_int(b.w);
+        for (int s = 1; s < Cw.ns; s++) {
+            const float w = Cw.w[s];
+            const float4 b = A.part_alb[s * ns + g], c = A.part_nrm[s * ns + g];
+            al = make_float4(al.x + b.x * w, al.y + b.y * w, al.z + b.z * w, 0.0f);
+            nr = make_float4(nr.x + c.x * w, nr.y + c.y * w, nr.z + c.z * w, 0.0f);
+            h += __float_as_int(b.w);
+        }
+        A.albedo[pixel] = al;
+        A.normal[pixel] = nr;
+        A.hits[pixel] = h;
     }
-    A.image[pixel] = im;
-    A.albedo[pixel] = al;
-    A.normal[pixel] = nr;
-    A.hits[pixel] = h;
 }
 
 // A chunk of a one-stream context (k = 1, the reference's single running mean): the chunk's
@@ -1449,6 +1467,22 @@ int zero_if_stale(jt_ctx* c) {
     c->stale = false;
     return JT_OK;
 }
+// the deferred AOV combine of the last launch (jt_ctx::aov_pending), before albedo, normal or
+// hits are read: jt_get_aovs, jt_synchronize, jt_get_device_buffers
+int finish_aovs(jt_ctx* c) {
+    if (!c->aov_pending) return JT_OK;
+    (void)hipSetDevice(c->device);
+    const int nblk = (int)(((long long)launch_tiles(c->P) * 64 + 255) / 256);
+    hipLaunchKernelGGL(jtk::combine_kernel<true>, dim3(nblk), dim3(256), 0, c->stream, c->P, c->A, c->aov_cw);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        c->failed = true;
+        return hip_fail(e, "AOV combine");
+    }
+    c->aov_pending = false;
+    return JT_OK;
+}
 }  // namespace
 
 int jt_reset(jt_ctx* c) {
@@ -1478,6 +1512,7 @@ int jt_reset(jt_ctx* c) {
     // tile share keeps the other tiles' pixels at zero for the reduce, and a context whose device
     // buffers were handed out is read in place, so those zero them now.
     c->stale = true;
+    c->aov_pending = false;
     c->pend0 = c->pend1 = 0;  // deferred samples are dropped with the state
     // a caller holding the device pointers (jt_get_device_buffers) sees the zeros at once
     if (c->P.tile_stride != 1 || c->exported) {
@@ -1602,8 +1637,10 @@ int trace_launch(jt_ctx* c, int32_t s0, int32_t s1, int32_t first) {
             DCombine cw{};
             cw.ns = (int)std::min(n, k);
             for (int j = 0; j < cw.ns; j++) cw.w[j] = (float)((double)((n - 1 - j) / k + 1) / (double)n);
-            if (nblk > 0) hipLaunchKernelGGL(combine_kernel, dim3(nblk), dim3(256), 0, c->stream, c->P, c->A, cw);
+            if (nblk > 0) hipLaunchKernelGGL(combine_kernel<false>, dim3(nblk), dim3(256), 0, c->stream, c->P, c->A, cw);
             if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "combine kernel launch");
+            c->aov_pending = nblk > 0;
+            c->aov_cw = cw;
         }
     }
     if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
@@ -1804,8 +1841,12 @@ int jt_get_aovs(jt_ctx* c, float* albedo, float* normal, int64_t* hits) {
     if (c->failed) return jt::fail(JT_ERR_STATE, "the running means are corrupt (a launch failed); jt_reset the context");
     for (jt_ctx* s : c->sub)
         if (const int st = zero_if_stale(s)) return st;
-    if (c->sub.empty())
+    for (jt_ctx* s : c->sub)
+        if (const int st = finish_aovs(s)) return st;
+    if (c->sub.empty()) {
         if (const int st = zero_if_stale(c)) return st;
+        if (const int st = finish_aovs(c)) return st;
+    }
     (void)hipSetDevice(c->device);
     const size_t np = (size_t)c->width * c->height;
     std::vector<float4> tmp(np);
@@ -1889,6 +1930,7 @@ int jt_get_device_buffers(jt_ctx* c, jt_device_buffers* out) {
     if (const int st = flush(c)) return st;
     if (!c->sub.empty()) return jt_get_device_buffers(c->sub[0], out);  // device 0's share
     if (const int st = zero_if_stale(c)) return st;
+    if (const int st = finish_aovs(c)) return st;
     c->exported = true;  // jt_reset now zeroes the buffers at once (the caller may read them)
     out->image = c->A.image;
     out->albedo = c->A.albedo;
@@ -1956,6 +1998,7 @@ int jt_synchronize(jt_ctx* c) {
         if (st != JT_OK) return st;
     }
     if (!c->sub.empty()) return JT_OK;
+    if (const int st = finish_aovs(c)) return st;
     (void)hipSetDevice(c->device);
     hipError_t e = hipStreamSynchronize(c->stream);
     return e == hipSuccess ? JT_OK : hip_fail(e, "hipStreamSynchronize");

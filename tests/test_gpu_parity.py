@@ -437,6 +437,34 @@ def test_device_buffer_view_is_the_running_mean(gpu, abi, lib, cornell_abi):
 
     out = reduce_running_means(dev, 3, 3, _OneRank, dst=0)
     np.testing.assert_allclose(out.cpu().numpy(), host, rtol=1e-6, atol=0)
+
+    # k > 1 streams combine the AOVs only when read: through the device pointers they are
+    # current after jt_synchronize, and equal jt_get_aovs (here after a second call that appends
+    # to the streams' means, so a stale combine would show)
+    def view(ptr, n, typestr):
+        class _V:
+            __cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False), "version": 3}
+        return torch.as_tensor(_V(), device="cuda:0")
+
+    sk = trace.make_trace_state(cornell_abi, bvh, lights, make_params(abi, resolution=48, samples=3, batch=3), lib)
+    assert sk.streams > 1, sk.describe()
+    bk = sk.device_buffers()
+    sk.trace_range(0, 2)
+    sk.trace_range(2, 3)
+    img_k = view(bk.image, H * W * 4, "<f4")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(img_k.cpu().numpy(), sk.get_image().reshape(-1))  # current at return
+    sk.synchronize()
+    torch.cuda.synchronize()
+    alb = view(bk.albedo, H * W * 4, "<f4").cpu().numpy().reshape(-1, 4)[:, :3]
+    nrm = view(bk.normal, H * W * 4, "<f4").cpu().numpy().reshape(-1, 4)[:, :3]
+    hit = view(bk.hits, H * W, "<i8").cpu().numpy()
+    a, n, h = sk.get_aovs()
+    np.testing.assert_array_equal(alb, a.reshape(-1, 3))
+    np.testing.assert_array_equal(nrm, n.reshape(-1, 3))
+    np.testing.assert_array_equal(hit, h.reshape(-1))
+    assert hit.sum() > 0
+    sk.close()
     # a reset zeroes the running means at once once their device pointers were handed out
     st.reset()
     torch.cuda.synchronize()
