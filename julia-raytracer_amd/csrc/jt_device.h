@@ -269,12 +269,30 @@ __device__ __forceinline__ v3 normalize(v3 a) {  // src/math.jl:71-78
 }
 __device__ __forceinline__ float length(v3 a) { return __builtin_sqrtf(dot(a, a)); }
 
-// Julia min/max for floats (base/math.jl): NaN-propagating, -0 < +0
+// Julia min/max for floats (base/math.jl): NaN-propagating, -0 < +0 — IEEE 754-2019
+// minimum/maximum, which gfx950 has as v_minimum3_f32 / v_maximum3_f32 (JT_NAN_PROP, one
+// instruction; the compare-and-select form otherwise). A NaN result may carry another payload than
+// Julia's (x's or y's): no decision and no stored value depends on a NaN's payload.
+#ifndef JT_NAN_PROP
+#define JT_NAN_PROP 1
+#endif
+__device__ __forceinline__ float jl_min3(float a, float b, float c) {
+    float r;
+    asm("v_minimum3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float jl_max3(float a, float b, float c) {
+    float r;
+    asm("v_maximum3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __device__ __forceinline__ float jl_min(float x, float y) {
+    if (JT_NAN_PROP) return jl_min3(x, y, y);
     bool c = (y < x) || (__builtin_signbit(y) && !__builtin_signbit(x));
     return c ? (__builtin_isnan(x) ? x : y) : (__builtin_isnan(y) ? y : x);
 }
 __device__ __forceinline__ float jl_max(float x, float y) {
+    if (JT_NAN_PROP) return jl_max3(x, y, y);
     bool c = (y > x) || (!__builtin_signbit(y) && __builtin_signbit(x));
     return c ? (__builtin_isnan(x) ? x : y) : (__builtin_isnan(y) ? y : x);
 }
@@ -292,7 +310,7 @@ __device__ __forceinline__ float jl_rcp(float x) {
     return 1.0f / x;
 }
 __device__ __forceinline__ int jl_clampi(int x, int lo, int hi) { return x > hi ? hi : (x < lo ? lo : x); }
-__device__ __forceinline__ float max3(v3 a) { return jl_max(jl_max(a.x, a.y), a.z); }
+__device__ __forceinline__ float max3(v3 a) { return JT_NAN_PROP ? jl_max3(a.x, a.y, a.z) : jl_max(jl_max(a.x, a.y), a.z); }
 
 #if JT_EXACT_MATH
 // Double-evaluated, once-rounded transcendentals (the float contract). The hot-path arguments
@@ -575,11 +593,23 @@ __device__ __forceinline__ bool slab_pass(float t0, float t1) { return (double)t
 // a = (bmin.x, bmax.x, bmin.y, bmax.y), b = (bmin.z, bmax.z, ..) (DNode). Scalar on purpose:
 // packed-FP32 (v_pk_add/v_pk_mul_f32) forms of these products measured 1.5 % slower on gfx950
 // (the broadcast ray operands then occupy register pairs).
+// JT_NAN_PROP (jl_min above): with Julia's min/max as single NaN-propagating instructions a NaN
+// slab value makes t0 or t1 NaN and the Float64 compare false, with no separate NaN test (three
+// v_cmp_o and their mask combines per box): the same decision as the form below for every input.
+// Measured against it (two runs each, interleaved, gpurun_out/r06nan2): cornellbox +1.5 %,
+// bathroom1 +1.6 %, ecosys +1.0 %, features2 +1.3 %.
 __device__ __forceinline__ bool intersect_bbox(v3 o, v3 dinv, float tmin, float tmax, const float4& a,
                                                const float4& b) {
     const float mx = (a.x - o.x) * dinv.x, Mx = (a.y - o.x) * dinv.x;
     const float my = (a.z - o.y) * dinv.y, My = (a.w - o.y) * dinv.y;
     const float mz = (b.x - o.z) * dinv.z, Mz = (b.y - o.z) * dinv.z;
+    if (JT_NAN_PROP) {
+        // t0 = max(min(mx, Mx), min(my, My), max(min(mz, Mz), tmin)), t1 likewise (the order of a
+        // max chain does not change its value; a NaN anywhere makes it NaN)
+        const float t0 = jl_max3(jl_min3(mx, Mx, Mx), jl_min3(my, My, My), jl_max3(jl_min3(mz, Mz, Mz), tmin, tmin));
+        const float t1 = jl_min3(jl_max3(mx, Mx, Mx), jl_max3(my, My, My), jl_min3(jl_max3(mz, Mz, Mz), tmax, tmax));
+        return slab_pass(t0, t1);
+    }
     bool nan = __builtin_isnan(mx) | __builtin_isnan(my) | __builtin_isnan(mz) | __builtin_isnan(Mx) |
                __builtin_isnan(My) | __builtin_isnan(Mz);
     float t0 = vmax3(vmin(mx, Mx), vmin(my, My), vmax(vmin(mz, Mz), tmin));

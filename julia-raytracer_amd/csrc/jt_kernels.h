@@ -726,14 +726,6 @@ __device__ __forceinline__ void wide_box(const float4& r0, const uint4& r1, cons
     a = make_float4(deq(r0.x, r1.x, sh, sx), deq(r0.x, r1.y, sh, sx), deq(r0.y, r1.z, sh, sy), deq(r0.y, r1.w, sh, sy));
     b = make_float4(deq(r0.z, r2.x, sh, sz), deq(r0.z, r2.y, sh, sz), 0.0f, 0.0f);
 }
-// intersect_bbox's decision from the six slab values (mx, Mx, my, My, mz, Mz), as intersect_bbox
-__device__ __forceinline__ bool slab_test(float mx, float Mx, float my, float My, float mz, float Mz, float tmin, float tmax) {
-    const bool nan = __builtin_isnan(mx) | __builtin_isnan(my) | __builtin_isnan(mz) | __builtin_isnan(Mx) |
-                     __builtin_isnan(My) | __builtin_isnan(Mz);
-    const float t0 = vmax3(vmin(mx, Mx), vmin(my, My), vmax(vmin(mz, Mz), tmin));
-    const float t1 = vmin3(vmax(mx, Mx), vmax(my, My), vmin(vmax(mz, Mz), tmax));
-    return !nan && slab_pass(t0, t1);
-}
 // Stack entries of the wide traversal (32 bits): a group — the children of record `index` still
 // to visit (bit 31 clear; bits 28-30 the record's flips for this ray, 24-27 the visit-order mask
 // of children whose boxes passed, 0-23 the record) — or an instance range (bit 31 set; bits 24-25
