@@ -1401,6 +1401,41 @@ struct DAccum {
     int nslot;  // launch tiles x 64 (the allocation's slots per stream)
 };
 
+// The kernels' argument layout (trace_kernel, trace_kernel_lds: by-value arguments in this order,
+// each at its natural alignment, as the AMDGPU kernarg segment lays them out).
+struct KArgs {
+    DScene S;
+    DParams P;
+    int s_begin, s_end;
+    DAccum A;
+};
+// JT_KARG_RELOAD: the launch's sample range and accumulator pointers are read from the kernel
+// argument segment (a scalar load through the kernarg pointer, laundered so it is not hoisted)
+// where they are used — at a work unit's fetch, an item's start and end — instead of being kept in
+// SGPRs across the path loop, where the register allocator spilled them to VGPR lanes and reloaded
+// them with v_readlane (a VALU instruction and a hazard wait each) in every shading phase.
+// Measured against keeping them (two runs each, interleaved, profiles/r06_ab/karg_reload_r06karg.txt):
+// cornellbox +3.1 %, bathroom1 1920x1080x64 +1.8 %, ecosys 3840x2160x8 +11 %, features2 -1.5 % (its
+// kernel's VGPR spills rose from 3 to 6), so the FT_MESH_ENV_QUAD kernel keeps them in registers.
+#ifndef JT_KARG_RELOAD
+#define JT_KARG_RELOAD 1
+#endif
+template <int F>
+__host__ __device__ constexpr bool karg_reload() {
+    // FT_MESH_ENV_QUAD (below): textures, attributes, materials, opacity, transforms, environments, quads
+    return JT_KARG_RELOAD && (F & ~(FT_LINL | FT_NOIL)) != (FT_TEX | FT_ATTR | FT_MAT | FT_OPAC | FT_XFORM | FT_ENV | FT_QUAD);
+}
+template <class T>
+__device__ __forceinline__ T karg(size_t off) {
+    typedef __attribute__((address_space(4))) const char* kptr;
+    kptr p = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const __attribute__((address_space(4))) T*)(p + off);
+}
+#define JT_A(f) (karg_reload<F>() ? karg<decltype(DAccum::f)>(offsetof(KArgs, A) + offsetof(DAccum, f)) : A.f)
+#define JT_SB (karg_reload<F>() ? karg<int>(offsetof(KArgs, s_begin)) : s_begin)
+#define JT_SE (karg_reload<F>() ? karg<int>(offsetof(KArgs, s_end)) : s_end)
+
 // Work units: (8x8 pixel tile t, stream slot q), fetched by whole waves from atomic counters, so
 // every wave stays busy until the launch's last units. The tiles are split into 8 bands of rows,
 // one per XCD: a wave drains its own XCD's band first (neighbouring pixels share that XCD's L2),
@@ -1554,7 +1589,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 const int bt0 = strips ? band * tiles_y / NBANDS * gx : band * tiles / NBANDS;
                 const int bn = strips ? (band + 1) * tiles_y / NBANDS * gx - bt0 : (band + 1) * tiles / NBANDS - bt0;
                 unsigned unit = 0;
-                if (lane == 0) unit = atomicAdd(A.work + band * BAND_STRIDE, 1u);
+                if (lane == 0) unit = atomicAdd(JT_A(work) + band * BAND_STRIDE, 1u);
                 unit = __builtin_amdgcn_readfirstlane(unit);
                 if (unit >= (unsigned)bn * (unsigned)nq) {
                     if (++band_k >= NBANDS) drained = true;
@@ -1580,23 +1615,23 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 if (i < P.width && j < P.height) {
                     item = (unsigned)(ut * 64 + l);
                     start = true;
-                    const int s = s_begin + uq;
+                    const int s = JT_SB + uq;
                     acc_i[11 * BLOCK] = s;
                     const int pixel = j * P.width + i;
                     float4 im = make_float4(0, 0, 0, 0), al = im, nr = im;
                     int h = 0;
                     if (s - P.first >= kstr) {  // the stream has earlier samples (an earlier launch)
                         if (P.lk == 0) {
-                            im = A.image[pixel];
-                            al = A.albedo[pixel];
-                            nr = A.normal[pixel];
-                            h = (int)A.hits[pixel];
+                            im = JT_A(image)[pixel];
+                            al = JT_A(albedo)[pixel];
+                            nr = JT_A(normal)[pixel];
+                            h = (int)JT_A(hits)[pixel];
                         } else {
-                            const size_t o = (size_t)((s - P.first) & (kstr - 1)) * (size_t)A.nslot +
+                            const size_t o = (size_t)((s - P.first) & (kstr - 1)) * (size_t)JT_A(nslot) +
                                              (size_t)item_slot(item, P);
-                            im = A.part_img[o];
-                            al = A.part_alb[o];
-                            nr = A.part_nrm[o];
+                            im = JT_A(part_img)[o];
+                            al = JT_A(part_alb)[o];
+                            nr = JT_A(part_nrm)[o];
                             h = __float_as_int(al.w);
                         }
                     }
@@ -1789,22 +1824,22 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
                 alive = false;
                 T.sp = -1;
                 const int sample = acc_i[11 * BLOCK];
-                if (sample + kstr >= s_end) {
+                if (sample + kstr >= JT_SE) {
                     // the item is complete: store its stream's means (plain stores: no other item
                     // of this launch reads them; the combine kernel runs after the launch)
                     const int pixel = item_pixel(item, P, tiles_x);
                     const float4 im = make_float4(acc[0], acc[BLOCK], acc[2 * BLOCK], acc[3 * BLOCK]);
                     if (P.lk == 0) {
-                        A.image[pixel] = im;
-                        A.albedo[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
-                        A.normal[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
-                        A.hits[pixel] = (long long)acc_i[10 * BLOCK];
+                        JT_A(image)[pixel] = im;
+                        JT_A(albedo)[pixel] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], 0.0f);
+                        JT_A(normal)[pixel] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
+                        JT_A(hits)[pixel] = (long long)acc_i[10 * BLOCK];
                     } else {
-                        const size_t o = (size_t)((sample - P.first) & (kstr - 1)) * (size_t)A.nslot +
+                        const size_t o = (size_t)((sample - P.first) & (kstr - 1)) * (size_t)JT_A(nslot) +
                                          (size_t)item_slot(item, P);
-                        A.part_img[o] = im;
-                        A.part_alb[o] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], __int_as_float(acc_i[10 * BLOCK]));
-                        A.part_nrm[o] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
+                        JT_A(part_img)[o] = im;
+                        JT_A(part_alb)[o] = make_float4(acc[4 * BLOCK], acc[5 * BLOCK], acc[6 * BLOCK], __int_as_float(acc_i[10 * BLOCK]));
+                        JT_A(part_nrm)[o] = make_float4(acc[7 * BLOCK], acc[8 * BLOCK], acc[9 * BLOCK], 0.0f);
                     }
                     item = ITEM_NONE;
                 } else {

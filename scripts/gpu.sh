@@ -20,7 +20,8 @@
 #   host                       the box's CPU description
 # workloads: cb (the headline, cornellbox path 1280x720x256), cb1 (config 1: naive 256x256x16),
 #   f2 (features2 1920x1080x512), b1 (bathroom1 1920x1080x1024), ec (ecosys 3840x2160 at 64 spp),
-#   ec8 (ecosys 3840x2160 at its 1/8 share, 512 spp), b1s/f2s/ecs (64/64/8 spp short forms);
+#   ec8 (ecosys 3840x2160 at its 1/8 share, 512 spp), b1s/f2s/ecs (64/64/8 spp short forms),
+#   f1s/m2s (features1 / materials2 1280x720x64: the general FT_ALL kernels);
 #   a suffix /N[gG] makes it rank 0's share of an N-rank run (G tile groups), e.g. cb/8, cb/8g8.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -44,6 +45,8 @@ wargs() {  # bench.py arguments of a workload name
         ec) a="--scene assets/scenes/ecosys/ecosys.json --width 3840 --height 2160 --spp 64" ;;
         ecs) a="--scene assets/scenes/ecosys/ecosys.json --width 3840 --height 2160 --spp 8" ;;
         ec8) a="--scene assets/scenes/ecosys/ecosys.json --width 3840 --height 2160 --spp 4096" ;;
+        f1s) a="--scene assets/scenes/features1/features1.json --width 1280 --height 720 --spp 64" ;;
+        m2s) a="--scene assets/scenes/materials2/materials2.json --width 1280 --height 720 --spp 64" ;;
         *) echo "unknown workload $base" >&2; return 1 ;;
     esac
     if [ -n "$share" ]; then
@@ -56,7 +59,7 @@ wargs() {  # bench.py arguments of a workload name
 steps() {  # timed steps / warmup of a workload: about 1-4 s of GPU time
     case ${1%%/*} in
         cb|cb1) echo "--steps 10 --warmup 2" ;;
-        f2|b1s|f2s|ecs) echo "--steps 3 --warmup 1" ;;
+        f2|b1s|f2s|ecs|f1s|m2s) echo "--steps 3 --warmup 1" ;;
         *) echo "--steps 1 --warmup 1" ;;
     esac
 }
