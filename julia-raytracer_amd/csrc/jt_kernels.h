@@ -1432,6 +1432,32 @@ __device__ __forceinline__ T karg(size_t off) {
     asm volatile("" : "+s"(p));
     return *(const __attribute__((address_space(4))) T*)(p + off);
 }
+// JT_KARG_SCENE (HBM-mode kernels, whose scene is the kernel argument itself): the shading phase
+// reads the scene's fields through the kernarg segment too (one scalar load per field used there,
+// re-issued every phase), instead of keeping every pointer the shading code needs live in SGPRs
+// across the traversal loop. Measured (two runs each, interleaved, profiles/r06_ab/
+// karg_scene_r06ks.txt): features2 1920x1080x64 +3.7 %, materials2 +1.4 %, features1 +0.9 %,
+// ecosys +0.8 %, cornellbox (LDS mode: not used) even; bathroom1 -2.1 %, so the FT_MESH kernel
+// keeps its scene in registers.
+#ifndef JT_KARG_SCENE
+#define JT_KARG_SCENE 1
+#endif
+template <bool NCACHE, int F>
+__host__ __device__ constexpr bool karg_scene() {
+    // FT_MESH (below): textures, attributes, materials, opacity, transforms
+    return NCACHE && JT_KARG_SCENE && (F & ~(FT_LINL | FT_NOIL)) != (FT_TEX | FT_ATTR | FT_MAT | FT_OPAC | FT_XFORM);
+}
+template <bool FROM_KARG>
+__device__ __forceinline__ const DScene& shade_scene(const DScene& S) {
+    if constexpr (FROM_KARG) {
+        typedef __attribute__((address_space(4))) const char* kptr;
+        kptr p = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(p));
+        return *(const DScene*)(const __attribute__((address_space(4))) DScene*)(p + offsetof(KArgs, S));
+    } else {
+        return S;
+    }
+}
 #define JT_A(f) (karg_reload<F>() ? karg<decltype(DAccum::f)>(offsetof(KArgs, A) + offsetof(DAccum, f)) : A.f)
 #define JT_SB (karg_reload<F>() ? karg<int>(offsetof(KArgs, s_begin)) : s_begin)
 #define JT_SE (karg_reload<F>() ? karg<int>(offsetof(KArgs, s_end)) : s_end)
@@ -1516,8 +1542,9 @@ __device__ __forceinline__ float stream_weight(const DParams& P, int s) {
 #endif
 
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, bool WIDE>
-__device__ __forceinline__ void trace_body_items(const DScene& S, const DParams& P, int s_begin, int s_end,
+__device__ __forceinline__ void trace_body_items(const DScene& S0, const DParams& P, int s_begin, int s_end,
                                                  const DAccum& A, int* stack) {
+    const DScene& S = S0;
     static_assert(lane_lds(F), "the per-lane item body keeps the lane's sample index in LDS");
     const int lane = threadIdx.x & 63;
     const int oslot = (int)blockIdx.x * BLOCK + (int)threadIdx.x;  // the lane's HBM stack-overflow area
@@ -1781,6 +1808,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S, const DParams&
         bool c_path = false, c_lq = false, c_ray = false;
         unsigned n_inl = 0;
         if (query_done<WIDE>(T)) {
+            const DScene& S = shade_scene<karg_scene<NCACHE, F>()>(S0);
             bool alive = true;
             // no light query ever leaves the shading phase (FT_LINL), or none exists (FT_NOIL)
             const bool light = SAMPLER == 1 && !LINL && st.phase == PH_LIGHT;
