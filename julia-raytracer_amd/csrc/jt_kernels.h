@@ -1458,6 +1458,25 @@ __device__ __forceinline__ const DScene& shade_scene(const DScene& S) {
         return S;
     }
 }
+// JT_KARG_SCENE_LDS: the same in the LDS-mode kernels, whose scene is the blob view of the kernel
+// argument (blob_scene): the shading phase rebuilds the view from the kernarg segment (the
+// cornellbox kernel's SGPR spills 53 -> 36; two runs each, profiles/r06_ab/karg_scene_lds_r06ksl.txt:
+// cornellbox +0.35 %, its 1/8 share +0.3 %, config 1 even)
+#ifndef JT_KARG_SCENE_LDS
+#define JT_KARG_SCENE_LDS 1
+#endif
+__device__ __forceinline__ DScene blob_scene(const DScene& S, const uint4* blob);
+__host__ __device__ constexpr size_t lds_stack_bytes(bool ovf, int ring, int need);
+template <bool NCACHE, int RING, bool OVF, int F>
+__device__ __forceinline__ DScene shade_scene_lds(const DScene& S0) {
+    if constexpr (!NCACHE && JT_KARG_SCENE_LDS) {
+        extern __shared__ uint4 dyn_lds[];
+        const DScene& K = shade_scene<true>(S0);
+        return blob_scene(K, dyn_lds + lds_stack_bytes(OVF, RING, K.stack_need) / 16);
+    } else {
+        return S0;
+    }
+}
 #define JT_A(f) (karg_reload<F>() ? karg<decltype(DAccum::f)>(offsetof(KArgs, A) + offsetof(DAccum, f)) : A.f)
 #define JT_SB (karg_reload<F>() ? karg<int>(offsetof(KArgs, s_begin)) : s_begin)
 #define JT_SE (karg_reload<F>() ? karg<int>(offsetof(KArgs, s_end)) : s_end)
@@ -1808,7 +1827,8 @@ __device__ __forceinline__ void trace_body_items(const DScene& S0, const DParams
         bool c_path = false, c_lq = false, c_ray = false;
         unsigned n_inl = 0;
         if (query_done<WIDE>(T)) {
-            const DScene& S = shade_scene<karg_scene<NCACHE, F>()>(S0);
+            const DScene SL = shade_scene_lds<NCACHE, RING, OVF, F>(S0);
+            const DScene& S = NCACHE ? shade_scene<karg_scene<NCACHE, F>()>(S0) : SL;
             bool alive = true;
             // no light query ever leaves the shading phase (FT_LINL), or none exists (FT_NOIL)
             const bool light = SAMPLER == 1 && !LINL && st.phase == PH_LIGHT;
