@@ -1458,6 +1458,29 @@ __device__ __forceinline__ const DScene& shade_scene(const DScene& S) {
         return S;
     }
 }
+// JT_KARG_PARAMS: the sample start and the shading phase read the render parameters (camera,
+// bounces, clamp, flags) through the kernarg segment too (the cornellbox kernel's SGPR spills
+// 36 -> 16, VGPR spills 1 -> 0). Two runs each (profiles/r06_ab/karg_params_r06kp.txt): cornellbox
+// +0.7 %, ecosys +1.0 %, features2 +0.9 %, materials2 +0.2 %; config 1's naive kernel -0.8 % and
+// bathroom1 -0.5 %, so the path-sampler kernels other than FT_MESH use it
+#ifndef JT_KARG_PARAMS
+#define JT_KARG_PARAMS 1
+#endif
+template <int SAMPLER, int F>
+__host__ __device__ constexpr bool karg_params_on() {
+    return JT_KARG_PARAMS && SAMPLER == 1 && (F & ~(FT_LINL | FT_NOIL)) != (FT_TEX | FT_ATTR | FT_MAT | FT_OPAC | FT_XFORM);
+}
+template <bool FROM_KARG>
+__device__ __forceinline__ const DParams& karg_params(const DParams& P) {
+    if constexpr (FROM_KARG) {
+        typedef __attribute__((address_space(4))) const char* kptr;
+        kptr p = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(p));
+        return *(const DParams*)(const __attribute__((address_space(4))) DParams*)(p + offsetof(KArgs, P));
+    } else {
+        return P;
+    }
+}
 // JT_KARG_SCENE_LDS: the same in the LDS-mode kernels, whose scene is the blob view of the kernel
 // argument (blob_scene): the shading phase rebuilds the view from the kernarg segment (the
 // cornellbox kernel's SGPR spills 53 -> 36; two runs each, profiles/r06_ab/karg_scene_lds_r06ksl.txt:
@@ -1561,9 +1584,10 @@ __device__ __forceinline__ float stream_weight(const DParams& P, int s) {
 #endif
 
 template <int SAMPLER, int RING, bool OVF, int COUNT, int F, bool NCACHE, bool WIDE>
-__device__ __forceinline__ void trace_body_items(const DScene& S0, const DParams& P, int s_begin, int s_end,
+__device__ __forceinline__ void trace_body_items(const DScene& S0, const DParams& P0, int s_begin, int s_end,
                                                  const DAccum& A, int* stack) {
     const DScene& S = S0;
+    const DParams& P = P0;
     static_assert(lane_lds(F), "the per-lane item body keeps the lane's sample index in LDS");
     const int lane = threadIdx.x & 63;
     const int oslot = (int)blockIdx.x * BLOCK + (int)threadIdx.x;  // the lane's HBM stack-overflow area
@@ -1703,6 +1727,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S0, const DParams
             const int sample = acc_i[11 * BLOCK];
             const int pixel = item_pixel(item, P, tiles_x);
             if (!ft_none(F)) acc[12 * BLOCK] = stream_weight(P, sample);
+            const DParams& P = karg_params<karg_params_on<SAMPLER, F>()>(P0);
             start_path<F>(P, pixel % P.width, pixel / P.width, pixel, sample, st);
             query_start<WIDE>(S, T, st.o, st.d, -1, stack);
             if (!WC) lds_count(1, true);
@@ -1827,6 +1852,7 @@ __device__ __forceinline__ void trace_body_items(const DScene& S0, const DParams
         bool c_path = false, c_lq = false, c_ray = false;
         unsigned n_inl = 0;
         if (query_done<WIDE>(T)) {
+            const DParams& P = karg_params<karg_params_on<SAMPLER, F>()>(P0);
             const DScene SL = shade_scene_lds<NCACHE, RING, OVF, F>(S0);
             const DScene& S = NCACHE ? shade_scene<karg_scene<NCACHE, F>()>(S0) : SL;
             bool alive = true;
